@@ -1,0 +1,258 @@
+"""Python front-end of the synthetic parquet writer (gen/libpqwrite.so).
+
+Test/bench input generation only.  `Column` describes one leaf column with its
+dense non-null values and (optional) def/rep levels; `write_file` returns the
+file bytes.  `config_*` build the BASELINE configs C1..C5 at any scale.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FLBA = range(8)
+PLAIN, RLE_DICTIONARY, DELTA_BINARY_PACKED = 0, 8, 5
+UNCOMPRESSED, SNAPPY = 0, 1
+REQUIRED, OPTIONAL, LIST = 0, 1, 2
+
+_lib = None
+
+
+class _PqwColumn(C.Structure):
+    _fields_ = [
+        ("name", C.c_char_p),
+        ("type", C.c_int32), ("type_length", C.c_int32), ("repetition", C.c_int32),
+        ("encoding", C.c_int32), ("codec", C.c_int32), ("page_version", C.c_int32),
+        ("rows_per_page", C.c_int32), ("min_rle", C.c_int32),
+        ("v2_uncompressed_flag", C.c_int32), ("reserved", C.c_int32),
+        ("dict_limit", C.c_int64),
+        ("values", C.c_void_p), ("offsets", C.c_void_p),
+        ("def_levels", C.c_void_p), ("rep_levels", C.c_void_p),
+        ("num_slots", C.c_int64), ("num_values", C.c_int64),
+    ]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(HERE, "libpqwrite.so")
+        if not os.path.exists(path):
+            raise RuntimeError("writer not built: run `make -C gen`")
+        L = C.CDLL(path)
+        L.pqw_write_file.argtypes = [C.POINTER(_PqwColumn), C.c_int, C.c_int64, C.c_int,
+                                     C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+        L.pqw_free.argtypes = [C.c_void_p]
+        L.pqw_hybrid_encode.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_void_p, C.c_int64]
+        L.pqw_hybrid_encode.restype = C.c_int64
+        L.pqw_dbp_encode64.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
+        L.pqw_dbp_encode64.restype = C.c_int64
+        L.pqw_dbp_encode32.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
+        L.pqw_dbp_encode32.restype = C.c_int64
+        L.pqw_snappy_compress.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
+        L.pqw_snappy_compress.restype = C.c_int64
+        _lib = L
+    return _lib
+
+
+class Column:
+    def __init__(self, name, ptype, values, *, type_length=0, repetition=REQUIRED, encoding=PLAIN,
+                 codec=UNCOMPRESSED, page_version=1, rows_per_page=20000, def_levels=None,
+                 rep_levels=None, offsets=None, dict_limit=0, min_rle=8, v2_uncompressed_flag=False):
+        self.name = name
+        self.ptype = ptype
+        self.type_length = type_length
+        self.repetition = repetition
+        self.encoding = encoding
+        self.codec = codec
+        self.page_version = page_version
+        self.rows_per_page = rows_per_page
+        self.min_rle = min_rle
+        self.dict_limit = dict_limit
+        self.v2_uncompressed_flag = v2_uncompressed_flag
+        self.values = np.ascontiguousarray(values)
+        self.offsets = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.int64)
+        self.def_levels = None if def_levels is None else np.ascontiguousarray(def_levels, dtype=np.uint8)
+        self.rep_levels = None if rep_levels is None else np.ascontiguousarray(rep_levels, dtype=np.uint8)
+        if self.offsets is not None:
+            self.num_values = len(self.offsets) - 1
+        elif ptype == FLBA:
+            self.num_values = self.values.nbytes // type_length
+        elif ptype == INT96:
+            self.num_values = self.values.nbytes // 12
+        else:
+            self.num_values = len(self.values)
+        self.num_slots = len(self.def_levels) if self.def_levels is not None else self.num_values
+
+    @property
+    def max_def(self):
+        return {REQUIRED: 0, OPTIONAL: 1, LIST: 3}[self.repetition]
+
+    @property
+    def max_rep(self):
+        return 1 if self.repetition == LIST else 0
+
+
+def write_file(columns, num_rows, row_groups=1):
+    L = lib()
+    arr = (_PqwColumn * len(columns))()
+    names = []
+    for i, c in enumerate(columns):
+        names.append(c.name.encode())
+        a = arr[i]
+        a.name = names[-1]
+        a.type, a.type_length, a.repetition = c.ptype, c.type_length, c.repetition
+        a.encoding, a.codec, a.page_version = c.encoding, c.codec, c.page_version
+        a.rows_per_page, a.min_rle = c.rows_per_page, c.min_rle
+        a.v2_uncompressed_flag = int(c.v2_uncompressed_flag)
+        a.dict_limit = c.dict_limit
+        a.values = c.values.ctypes.data if c.values.size else None
+        a.offsets = c.offsets.ctypes.data if c.offsets is not None else None
+        a.def_levels = c.def_levels.ctypes.data if c.def_levels is not None else None
+        a.rep_levels = c.rep_levels.ctypes.data if c.rep_levels is not None else None
+        a.num_slots, a.num_values = c.num_slots, c.num_values
+    out = C.c_void_p()
+    n = C.c_int64()
+    rc = L.pqw_write_file(arr, len(columns), num_rows, row_groups, C.byref(out), C.byref(n))
+    if rc != 0:
+        raise ValueError("pqw_write_file failed: %d" % rc)
+    data = C.string_at(out, n.value)
+    L.pqw_free(out)
+    return data
+
+
+def hybrid_encode(values, width, min_rle=8):
+    v = np.ascontiguousarray(values, dtype=np.uint32)
+    cap = len(v) * 8 + 64
+    out = np.zeros(cap, dtype=np.uint8)
+    n = lib().pqw_hybrid_encode(v.ctypes.data, len(v), width, min_rle, out.ctypes.data, cap)
+    assert n >= 0
+    return out[:n].tobytes()
+
+
+def dbp_encode(values, bits=64):
+    v = np.ascontiguousarray(values, dtype=np.int64 if bits == 64 else np.int32)
+    cap = len(v) * 10 + 1024
+    out = np.zeros(cap, dtype=np.uint8)
+    fn = lib().pqw_dbp_encode64 if bits == 64 else lib().pqw_dbp_encode32
+    n = fn(v.ctypes.data, len(v), out.ctypes.data, cap)
+    assert n >= 0
+    return out[:n].tobytes()
+
+
+def snappy_compress(data: bytes):
+    src = np.frombuffer(data, dtype=np.uint8)
+    cap = len(data) + len(data) // 6 + 64
+    out = np.zeros(cap, dtype=np.uint8)
+    n = lib().pqw_snappy_compress(src.ctypes.data if len(src) else None, len(src), out.ctypes.data, cap)
+    assert n >= 0
+    return out[:n].tobytes()
+
+
+# --------------------------------------------------------------------------
+# BASELINE configs (BASELINE.md "Configs as concrete synthetic inputs")
+# --------------------------------------------------------------------------
+
+def splitmix64(seed, n):
+    x = (np.arange(1, n + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(seed))
+    z = x.copy()
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def config_c1(rows=10_000_000, rows_per_page=20000, seed=1):
+    """C1: required int64, PLAIN, UNCOMPRESSED, one row group, V1."""
+    vals = splitmix64(seed, rows).view(np.int64)
+    col = Column("c1", INT64, vals, rows_per_page=rows_per_page)
+    return write_file([col], rows), {"rows": rows}
+
+
+def config_c2(rows=100_000_000, bits=8, null_frac=0.10, run_heavy=False, rows_per_page=20000, seed=2,
+              page_version=1, codec=UNCOMPRESSED):
+    """C2: optional int32, RLE_DICTIONARY with D = 2^bits entries, ~10% nulls, V1."""
+    rng = np.random.default_rng(seed + bits)
+    d = 1 << bits
+    dict_vals = rng.integers(-2**31, 2**31 - 1, size=d, dtype=np.int64).astype(np.int32)
+    dict_vals[: min(d, 1)] = 0
+    defs = (rng.random(rows) >= null_frac).astype(np.uint8)
+    nn = int(defs.sum())
+    if run_heavy:
+        lens = rng.geometric(1.0 / 16, size=nn // 4 + 16)
+        keys = rng.integers(0, d, size=len(lens))
+        idx = np.repeat(keys, lens)[:nn]
+        if len(idx) < nn:
+            idx = np.concatenate([idx, rng.integers(0, d, size=nn - len(idx))])
+    else:
+        idx = rng.integers(0, d, size=nn)
+        # make sure every dictionary entry appears so the index width is `bits`
+        idx[: min(d, nn)] = np.arange(min(d, nn))
+    vals = dict_vals[idx]
+    col = Column("c2", INT32, vals, repetition=OPTIONAL, encoding=RLE_DICTIONARY, def_levels=defs,
+                 rows_per_page=rows_per_page, page_version=page_version, codec=codec)
+    return write_file([col], rows), {"rows": rows, "non_null": nn, "bits": bits}
+
+
+def config_c3(rows=200_000_000, rows_per_page=20000, seed=3, codec=SNAPPY):
+    """C3: int64 timestamps, DELTA_BINARY_PACKED, V2, SNAPPY (is_compressed=true)."""
+    rng = np.random.default_rng(seed)
+    deltas = 1000 + rng.integers(-50, 51, size=rows, dtype=np.int64)
+    deltas[0] = 0
+    vals = np.int64(1_600_000_000_000_000) + np.cumsum(deltas)
+    col = Column("ts", INT64, vals, encoding=DELTA_BINARY_PACKED, codec=codec, page_version=2,
+                 rows_per_page=rows_per_page)
+    return write_file([col], rows), {"rows": rows}
+
+
+def make_vocab(n, seed, lo=4, hi=32):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(lo, hi + 1, size=n)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(lens)
+    chars = rng.integers(97, 123, size=int(offs[-1]), dtype=np.uint8)
+    # make words unique by stamping the index into the first 4 bytes
+    for i in range(n):
+        chars[offs[i]:offs[i] + 4] = np.frombuffer(np.uint32(i).tobytes(), dtype=np.uint8) % 26 + 65
+    return chars, offs
+
+
+def config_c4(rows=50_000_000, vocab=65536, rows_per_page=20000, seed=4, dict_limit=1 << 20, codec=SNAPPY):
+    """C4: required STRING, dictionary then PLAIN fallback after 1 MiB of dictionary, SNAPPY, V1."""
+    rng = np.random.default_rng(seed)
+    chars, offs = make_vocab(vocab, seed)
+    ranks = rng.zipf(1.1, size=rows * 2)
+    ranks = ranks[ranks <= vocab][:rows] - 1
+    while len(ranks) < rows:
+        more = rng.zipf(1.1, size=rows)
+        ranks = np.concatenate([ranks, more[more <= vocab][: rows - len(ranks)] - 1])
+    lens = (offs[1:] - offs[:-1])[ranks]
+    out_offs = np.zeros(rows + 1, dtype=np.int64)
+    out_offs[1:] = np.cumsum(lens)
+    starts = offs[:-1][ranks]
+    total = int(out_offs[-1])
+    # gather chars
+    idx = np.repeat(starts - out_offs[:-1], lens) + np.arange(total, dtype=np.int64)
+    out_chars = chars[idx]
+    col = Column("s", BYTE_ARRAY, out_chars, offsets=out_offs, encoding=RLE_DICTIONARY, codec=codec,
+                 rows_per_page=rows_per_page, dict_limit=dict_limit)
+    return write_file([col], rows), {"rows": rows}
+
+
+def config_c2_family(rows=100_000_000, bits_list=(1, 2, 4, 8, 12, 16, 20), null_frac=0.10, rows_per_page=20000,
+                     seed=2):
+    """C2 at every index width: one file per width sharing the null pattern and
+    the (masked) uniform index draw.  Yields (bits, file_bytes, expected) where
+    expected = (def_levels u8[rows], dense int32 values)."""
+    rng = np.random.default_rng(seed)
+    defs = (rng.random(rows) >= null_frac).astype(np.uint8)
+    nn = int(defs.sum())
+    raw = rng.integers(0, 1 << 20, size=nn, dtype=np.int64)
+    dict_all = rng.integers(-2**31, 2**31 - 1, size=1 << 20, dtype=np.int64).astype(np.int32)
+    for bits in bits_list:
+        d = 1 << bits
+        idx = raw & (d - 1)
+        idx[: min(d, nn)] = np.arange(min(d, nn))
+        vals = dict_all[:d][idx]
+        col = Column("c2", INT32, vals, repetition=OPTIONAL, encoding=RLE_DICTIONARY, def_levels=defs,
+                     rows_per_page=rows_per_page)
+        yield bits, write_file([col], rows), (defs, vals)

@@ -1,0 +1,262 @@
+/*
+ * pqgpu.h — C ABI of the MI355X (gfx950) Parquet column-chunk decoder.
+ *
+ * This is the drop-in boundary for parquet-go's page-decode path
+ * (fraugster/parquet-go v0.2.1, mounted read-only at /root/reference).  Every
+ * entry point below names the reference interface it replaces.  Signatures use
+ * plain pointers and sizes only (no torch / HIP types), so a cgo, ctypes or
+ * JNI binding can call them directly.
+ *
+ * Two libraries implement (parts of) this header:
+ *   libpqgpu.so   (parquet-go_amd/csrc)  the product: HIP kernels + host runtime
+ *   liboracle.so  (oracle/)              TEST INFRASTRUCTURE ONLY: the CPU
+ *                                        restatement of the reference algorithm
+ *                                        (pqo_* symbols), used as the parity checker.
+ *
+ * Semantics: a "chunk job" is one column chunk (ColumnChunk / ColumnMetaData of
+ * one row group).  Decoding a job is what the reference does in
+ *   readChunk      chunk_reader.go:314-378   (seek, level-decoder factories)
+ *   readPages      chunk_reader.go:206-284   (page-header walk, dict page, V1/V2)
+ *   readPageData   chunk_reader.go:380-402   (per page readValues)
+ * and the per-page outputs are exactly pageReader.readValues
+ * (interfaces.go:10-17; page_v1.go:27-55, page_v2.go:26-54):
+ *   rLevels[numValues], dLevels[numValues], values[:notNull]
+ * concatenated over the data pages of the chunk in file order (spec-correct
+ * stitching; see DESIGN.md "Quirk policy" for the reference's Q1/Q2 defects).
+ */
+#ifndef PQGPU_H
+#define PQGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- parquet.thrift enums (reference parquet/parquet.go: Type, Encoding :343,
+ *      CompressionCodec :442, PageType :525) ------------------------------- */
+enum {
+  PQG_BOOLEAN = 0,
+  PQG_INT32 = 1,
+  PQG_INT64 = 2,
+  PQG_INT96 = 3,
+  PQG_FLOAT = 4,
+  PQG_DOUBLE = 5,
+  PQG_BYTE_ARRAY = 6,
+  PQG_FIXED_LEN_BYTE_ARRAY = 7
+};
+enum {
+  PQG_ENC_PLAIN = 0,
+  PQG_ENC_PLAIN_DICTIONARY = 2,
+  PQG_ENC_RLE = 3,
+  PQG_ENC_BIT_PACKED = 4,
+  PQG_ENC_DELTA_BINARY_PACKED = 5,
+  PQG_ENC_DELTA_LENGTH_BYTE_ARRAY = 6,
+  PQG_ENC_DELTA_BYTE_ARRAY = 7,
+  PQG_ENC_RLE_DICTIONARY = 8
+};
+enum {
+  PQG_CODEC_UNCOMPRESSED = 0,
+  PQG_CODEC_SNAPPY = 1,
+  PQG_CODEC_GZIP = 2
+};
+enum {
+  PQG_PAGE_DATA = 0,
+  PQG_PAGE_INDEX = 1,
+  PQG_PAGE_DICTIONARY = 2,
+  PQG_PAGE_DATA_V2 = 3
+};
+
+/* ---- status codes --------------------------------------------------------
+ * The reference returns a Go error (wrapped with github.com/pkg/errors) and
+ * treats ANY error inside readPages/readPageData as fatal for the row group.
+ * Parity is defined on error/no-error per page and per chunk; the class below
+ * is this library's own classification, identical between libpqgpu and the
+ * oracle (both follow the same cited reference lines). */
+enum {
+  PQG_OK = 0,
+  PQG_ERR_EOF = -1,           /* io.EOF / io.ErrUnexpectedEOF inside a stream       */
+  PQG_ERR_THRIFT = -2,        /* PageHeader thrift-compact decode failed            */
+  PQG_ERR_PAGE_HEADER = -3,   /* missing sub-header, negative count/size            */
+  PQG_ERR_SIZE = -4,          /* block shorter than compressed size / size mismatch */
+  PQG_ERR_SNAPPY = -5,        /* snappy: corrupt input                              */
+  PQG_ERR_RLE = -6,           /* hybrid: empty run, RLE value too large, bad varint */
+  PQG_ERR_DICT_INDEX = -7,    /* dict: invalid index                                */
+  PQG_ERR_BIT_WIDTH = -8,     /* dict/delta: invalid bit width                      */
+  PQG_ERR_DELTA = -9,         /* DELTA_BINARY_PACKED header/stream invalid          */
+  PQG_ERR_UNSUPPORTED = -10,  /* encoding / codec / type / page type                */
+  PQG_ERR_DICT_PAGE = -11,    /* second dictionary page                             */
+  PQG_ERR_BYTE_ARRAY = -12,   /* bytearray/plain: negative length                   */
+  PQG_ERR_LEVELS = -13,       /* level decoder not initialised (V2, zero length)    */
+  PQG_ERR_CAPACITY = -20,     /* internal: arena too small; host grows and retries  */
+  PQG_ERR_INVALID_ARG = -21,
+  PQG_ERR_HIP = -22,
+  PQG_ERR_METADATA = -23,     /* footer / FileMetaData problems                      */
+  PQG_ERR_NOT_BUILT = -24
+};
+
+/* page_info.flags */
+enum {
+  PQG_PAGE_FLAG_INT96_NIL = 1   /* Q8: truncated final INT96 value left nil by the
+                                   reference (type_int96.go:21-42); bytes are 0 */
+};
+
+/* ---- column / chunk description ----------------------------------------- */
+
+/* What readChunk learns from the schema (schema.go:789-894) and the chunk's
+ * ColumnMetaData (parquet.go ColumnMetaData). */
+typedef struct pqg_column_desc {
+  int32_t physical_type; /* PQG_INT32 ...                                        */
+  int32_t type_length;   /* FIXED_LEN_BYTE_ARRAY length; -1 = unset (nil)        */
+  int32_t max_def;       /* Column.MaxDefinitionLevel()  (0..255)                */
+  int32_t max_rep;       /* Column.MaxRepetitionLevel()  (0..255)                */
+  int32_t codec;         /* ColumnMetaData.codec                                 */
+  int32_t flags;         /* bit0: unsigned (uint32/uint64 Go type; bits identical) */
+} pqg_column_desc;
+
+/* One column chunk to decode.  `data` points at the chunk's first page
+ * (DictionaryPageOffset when set, else DataPageOffset — chunk_reader.go:332-340).
+ * For pqg_decode_chunks it is a DEVICE pointer (bytes resident in HBM); for the
+ * oracle it is a host pointer. */
+typedef struct pqg_chunk_job {
+  pqg_column_desc col;
+  const uint8_t* data;
+  int64_t data_len;              /* readable bytes at data (>= total_compressed_size) */
+  int64_t total_compressed_size; /* ColumnMetaData.total_compressed_size              */
+  int64_t data_page_offset;      /* DataPageOffset - first-page offset (>= 0)          */
+  int64_t num_values_hint;       /* ColumnMetaData.num_values (capacity hint only)     */
+  int64_t total_uncompressed_size; /* ColumnMetaData.total_uncompressed_size (hint)     */
+  int32_t has_dict_page_offset;  /* ColumnMetaData.DictionaryPageOffset != nil         */
+  int32_t reserved;
+} pqg_chunk_job;
+
+/* Decoded column chunk.  Fixed-width physical types (INT32/INT64/INT96/FLOAT/
+ * DOUBLE/FLBA>0/BOOLEAN) store values densely, little endian, `value_width`
+ * bytes each (BOOLEAN: one byte 0/1).  BYTE_ARRAY (and FLBA with length 0)
+ * store chars in `values` and num_values+1 int64 offsets.  Pointers are DEVICE
+ * pointers for libpqgpu (owned by the ctx, valid until the next decode on that
+ * ctx or pqg_ctx_destroy) and malloc'ed host pointers for the oracle. */
+typedef struct pqg_chunk_result {
+  int32_t status;      /* first error in reference order (read phase, then decode) */
+  int32_t error_page;  /* index into the page list of the failing page, -1 if none */
+  int32_t num_pages;   /* pages seen (dictionary page included)                    */
+  int32_t value_width; /* bytes per value; 0 = variable length (offsets)           */
+  int64_t num_slots;   /* Σ data-page num_values  (= level entries)                */
+  int64_t num_values;  /* Σ notNull                                                */
+  int64_t values_bytes;
+  uint8_t* def_levels; /* num_slots bytes, NULL when max_def == 0                  */
+  uint8_t* rep_levels; /* num_slots bytes, NULL when max_rep == 0                  */
+  uint8_t* values;
+  int64_t* offsets;    /* variable-length values only                              */
+} pqg_chunk_result;
+
+/* Per page bookkeeping (dictionary page included, in file order). */
+typedef struct pqg_page_info {
+  int64_t header_offset;     /* relative to job.data                    */
+  int64_t payload_offset;    /* first byte after the thrift header      */
+  int64_t slot_offset;       /* Σ num_values of preceding data pages    */
+  int64_t value_offset;      /* Σ not_null  of preceding data pages     */
+  int32_t page_type;
+  int32_t encoding;
+  int32_t num_values;        /* header NumValues                        */
+  int32_t not_null;          /* #(dLevel == maxD)                        */
+  int32_t compressed_size;
+  int32_t uncompressed_size;
+  int32_t def_len;           /* V2 DefinitionLevelsByteLength           */
+  int32_t rep_len;           /* V2 RepetitionLevelsByteLength           */
+  int32_t def_encoding;      /* V1 definition_level_encoding            */
+  int32_t rep_encoding;
+  int32_t status;
+  int32_t flags;             /* PQG_PAGE_FLAG_*                          */
+} pqg_page_info;
+
+/* ======================= libpqgpu (product) =============================== */
+
+typedef struct pqg_ctx pqg_ctx;
+
+/* One context per GPU; owns a HIP stream and grow-only device arenas.
+ * (No reference counterpart: parquet-go's reader is one goroutine per FileReader.) */
+int pqg_ctx_create(int device, pqg_ctx** out);
+void pqg_ctx_destroy(pqg_ctx* ctx);
+const char* pqg_status_string(int status);
+
+/* Device memory helpers for callers without their own allocator (cgo). */
+int pqg_device_alloc(pqg_ctx* ctx, int64_t bytes, void** dptr);
+int pqg_device_free(pqg_ctx* ctx, void* dptr);
+int pqg_memcpy_h2d(pqg_ctx* ctx, void* dst, const void* src, int64_t bytes);
+int pqg_memcpy_d2h(pqg_ctx* ctx, void* dst, const void* src, int64_t bytes);
+
+/* Decode a batch of column chunks already resident in HBM.  Replaces, for
+ * every job, readChunk+readPages+readPageData (chunk_reader.go:206-402) and the
+ * valuesDecoder / levelDecoder implementations they call (interfaces.go:28-38,
+ * hybrid_decoder.go:17-28).  Enqueues work on the ctx stream and returns;
+ * pqg_sync waits and fills `results` (n_jobs entries). */
+int pqg_decode_chunks_async(pqg_ctx* ctx, const pqg_chunk_job* jobs, int n_jobs);
+int pqg_sync(pqg_ctx* ctx, pqg_chunk_result* results, int n_jobs);
+/* Convenience: async + sync. */
+int pqg_decode_chunks(pqg_ctx* ctx, const pqg_chunk_job* jobs, int n_jobs,
+                      pqg_chunk_result* results);
+
+/* After pqg_sync: page table of job `job` (host copy).  Returns pages written
+ * or a negative status. */
+int pqg_get_pages(pqg_ctx* ctx, int job, pqg_page_info* out, int cap);
+
+/* Kernel timing of the last decode (HIP events on the ctx stream), in ms:
+ * out[0] = whole pipeline, out[1..] = per stage. Returns the
+ * number of entries written. */
+int pqg_last_timings(pqg_ctx* ctx, float* out, int cap);
+
+/* Optional: run `iters` back-to-back decodes of the same jobs on the ctx
+ * stream and return the device time in ms (used by bench.py).  */
+int pqg_bench_decode(pqg_ctx* ctx, const pqg_chunk_job* jobs, int n_jobs, int iters,
+                     float* ms_total, float* ms_stage, int stage_cap);
+
+/* ---- host-side planner: footer / schema (file_meta.go:14-62, schema.go) --- */
+typedef struct pqg_file pqg_file;
+
+typedef struct pqg_column_info {
+  pqg_column_desc desc;
+  char path[256];        /* dotted flat name (schema.go flatName) */
+} pqg_column_info;
+
+typedef struct pqg_chunk_meta {
+  int64_t start;                 /* DictionaryPageOffset if set else DataPageOffset */
+  int64_t total_compressed_size;
+  int64_t total_uncompressed_size;
+  int64_t data_page_offset;      /* absolute */
+  int64_t num_values;
+  int32_t has_dict_page_offset;
+  int32_t codec;
+  int32_t type;                  /* ColumnMetaData.type */
+  int32_t reserved;
+} pqg_chunk_meta;
+
+/* Parse a whole parquet file held in host memory: PAR1 magic at both ends,
+ * footer length, thrift FileMetaData, schema → leaf columns with maxD/maxR. */
+int pqg_file_open(const uint8_t* file, int64_t len, pqg_file** out);
+void pqg_file_close(pqg_file* f);
+int pqg_file_num_columns(const pqg_file* f);
+int pqg_file_num_row_groups(const pqg_file* f);
+int64_t pqg_file_num_rows(const pqg_file* f);
+int pqg_file_column(const pqg_file* f, int col, pqg_column_info* out);
+int pqg_file_chunk(const pqg_file* f, int row_group, int col, pqg_chunk_meta* out);
+int64_t pqg_file_row_group_rows(const pqg_file* f, int row_group);
+
+/* ======================= oracle (TEST INFRASTRUCTURE) ===================== */
+/* Implemented only by oracle/liboracle.so.  Host pointers everywhere. */
+int pqo_decode_chunk(const pqg_chunk_job* job, pqg_chunk_result* res,
+                     pqg_page_info* pages, int page_cap, int* n_pages);
+void pqo_free_result(pqg_chunk_result* res);
+int pqo_unpack8_32(const uint8_t* data, int width, int32_t* out8);
+int pqo_unpack8_64(const uint8_t* data, int width, int64_t* out8);
+/* hybrid RLE/bit-pack: decode `count` values of `width` bits (levelDecoder.next) */
+int pqo_hybrid_decode(const uint8_t* buf, int64_t len, int width, int64_t count, int32_t* out);
+int pqo_snappy_decode(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int64_t* out_len);
+int pqo_delta_decode64(const uint8_t* buf, int64_t len, int64_t count, int64_t* out);
+int pqo_delta_decode32(const uint8_t* buf, int64_t len, int64_t count, int32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PQGPU_H */

@@ -1,0 +1,100 @@
+// pqg_common.h — device/host shared records of the gfx950 decode pipeline.
+//
+// Layout in HBM (one ctx, one batch of chunk jobs):
+//   JobDev[n_jobs]             per column chunk: inputs, arena regions, results
+//   PageDev[page_cap_total]    page table; job j owns [page_base, page_base+page_cap)
+//   level arena  (u8)          def/rep levels, job j at slot_base (num_slots each)
+//   value arena  (bytes)       dense values[:nn], job j at value_base
+//   scratch arena (bytes)      decompressed (snappy) page blocks, job j at scratch_base
+//   offsets arena (i64)        variable-length value offsets
+#pragma once
+#include <stdint.h>
+
+#ifndef __HIPCC__
+#ifndef __host__
+#define __host__
+#define __device__
+#define __forceinline__ inline
+#endif
+#endif
+
+namespace pqg {
+
+enum : int32_t {
+  kOK = 0,
+  kEOF = -1,
+  kTHRIFT = -2,
+  kPAGE_HEADER = -3,
+  kSIZE = -4,
+  kSNAPPY = -5,
+  kRLE = -6,
+  kDICT_INDEX = -7,
+  kBIT_WIDTH = -8,
+  kDELTA = -9,
+  kUNSUPPORTED = -10,
+  kDICT_PAGE = -11,
+  kBYTE_ARRAY = -12,
+  kLEVELS = -13,
+  kCAPACITY = -20,
+};
+
+// Header fields of one page (thrift PageHeader subset, parquet.go:5794-5803).
+struct PageHdr {
+  int32_t type, usize, csize;
+  int32_t num_values, encoding, def_enc, rep_enc;   // DataPageHeader / Dict / V2
+  int32_t v2_def_len, v2_rep_len;
+  int32_t has_dph, has_dict, has_v2;
+  int32_t hlen;  // header bytes
+};
+
+struct PageDev {
+  int64_t header_offset;   // relative to job data
+  int64_t payload_offset;  // header_offset + hlen
+  int64_t slot_offset;     // Σ num_values of preceding data pages (job-relative)
+  int64_t value_offset;    // Σ not_null of preceding data pages (job-relative)
+  int64_t scratch_offset;  // decompressed block (job-relative), -1 = not compressed
+  // resolved streams (absolute device pointers, filled by the level stage)
+  const uint8_t* block;    // values block (V1: the whole page body)
+  int64_t block_len;
+  const uint8_t* rep;  int64_t rep_n;
+  const uint8_t* def;  int64_t def_n;
+  const uint8_t* val;  int64_t val_n;
+  int32_t page_type, encoding, num_values, csize, usize;
+  int32_t def_len, rep_len, def_enc, rep_enc;
+  int32_t job;
+  int32_t read_status;     // error of the reference's read phase (readPages)
+  int32_t decode_status;   // error of readValues (readPageData)
+  int32_t not_null;
+  int32_t flags;
+  int32_t dict_width;      // RLE_DICTIONARY: index bit width byte
+  int32_t pad;
+};
+
+struct JobDev {
+  // ---- inputs
+  const uint8_t* data;
+  int64_t data_len, tcs, data_page_offset;
+  int32_t type, type_length, max_def, max_rep, codec, has_dict_off;
+  int32_t value_width;     // bytes per value, 0 = variable
+  int32_t page_cap;
+  int64_t page_base;
+  int64_t slot_cap, slot_base;        // level arenas (bytes == slots)
+  int64_t value_cap, value_base;      // value arena (bytes)
+  int64_t scratch_cap, scratch_base;  // scratch arena (bytes)
+  int64_t offs_cap, offs_base;        // offsets arena (entries)
+  // ---- results (device written)
+  int32_t num_pages;       // pages found by the walk (may exceed page_cap)
+  int32_t dict_page;       // page index of the dictionary page, -1 if none
+  int32_t scan_status;     // first read-phase error found by the walk
+  int32_t status;          // final chunk status
+  int32_t error_page;
+  int32_t n_out_pages;     // pages reported (truncated at first read error)
+  int64_t num_slots, num_values, values_bytes;
+  int64_t need_scratch;    // Σ usize of compressed blocks
+  const uint8_t* dict_data;  // dictionary entries (fixed width) or chars (var)
+  int64_t dict_count, dict_len;
+  const int64_t* dict_offs;  // variable-length dictionary offsets (count+1)
+  int32_t flags, pad;
+};
+
+}  // namespace pqg

@@ -1,0 +1,140 @@
+// pqg_device.h — wave-level building blocks of the gfx950 decoder.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "pqg_common.h"
+
+namespace pqg {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+// Bounds-checked byte read of a device buffer.
+__device__ __forceinline__ int get_byte(const uint8_t* p, int64_t n, int64_t i) {
+  return (i >= 0 && i < n) ? (int)p[i] : -1;
+}
+
+// Read 8 bytes little endian starting at byte i of [p, p+n); bytes at or
+// beyond `valid` read as 0 (Q5 zero padding), bytes beyond n are never touched.
+// Fast path: the aligned dwords covering [i, i+8) all contain a readable byte,
+// so they lie on pages that are mapped.
+__device__ __forceinline__ uint64_t load_u64_masked(const uint8_t* p, int64_t n, int64_t i, int64_t valid) {
+  int64_t lim = valid < n ? valid : n;
+  if (i >= 0 && i + 8 <= lim) {
+    uintptr_t a = (uintptr_t)(p + i);
+    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+    int sh = (int)(a & 3) * 8;
+    uint64_t lo = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+    if (sh == 0) return lo;
+    uint64_t hi = (uint64_t)q[2];
+    return (lo >> sh) | (hi << (64 - sh));
+  }
+  uint64_t v = 0;
+  for (int k = 0; k < 8; k++) {
+    int64_t j = i + k;
+    if (j >= 0 && j < lim) v |= (uint64_t)p[j] << (8 * k);
+  }
+  return v;
+}
+
+// Extract `w` (<= 32) bits at bit offset `bit` of stream [p, p+valid).
+__device__ __forceinline__ uint32_t extract_bits32(const uint8_t* p, int64_t n, int64_t valid, int64_t bit, int w) {
+  if (w == 0) return 0;
+  uint64_t x = load_u64_masked(p, n, bit >> 3, valid);
+  x >>= (bit & 7);
+  return (uint32_t)(x & ((w == 32) ? 0xffffffffull : ((1ull << w) - 1)));
+}
+
+// Extract `w` (<= 64) bits.
+__device__ __forceinline__ uint64_t extract_bits64(const uint8_t* p, int64_t n, int64_t valid, int64_t bit, int w) {
+  if (w == 0) return 0;
+  int64_t byte = bit >> 3;
+  int sh = (int)(bit & 7);
+  uint64_t lo = load_u64_masked(p, n, byte, valid);
+  uint64_t v = lo >> sh;
+  if (sh + w > 64) {
+    uint64_t hi = load_u64_masked(p, n, byte + 8, valid);
+    v |= hi << (64 - sh);
+  }
+  return w == 64 ? v : (v & ((1ull << w) - 1));
+}
+
+// ---------------------------------------------------------------------------
+// Wave-wide reductions / scans (64 lanes).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t wave_sum(int64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int64_t wave_min(int64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    int64_t t = __shfl_xor(v, o, 64);
+    v = t < v ? t : v;
+  }
+  return v;
+}
+// inclusive scan of uint64 (wrapping)
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
+  int l = lane_id();
+  for (int o = 1; o < 64; o <<= 1) {
+    uint64_t t = __shfl_up(v, o, 64);
+    if (l >= o) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ int64_t wave_excl_scan_i64(int64_t v, int64_t* total) {
+  int l = lane_id();
+  int64_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t t = __shfl_up(x, o, 64);
+    if (l >= o) x += t;
+  }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+// ---------------------------------------------------------------------------
+// LDS byte window over a device stream, refilled cooperatively by the wave.
+// All lanes call get() with the same position (wave-uniform control flow).
+// ---------------------------------------------------------------------------
+constexpr int kWin = 1024;
+constexpr int64_t kFarAway = -((int64_t)1 << 62);
+
+struct Window {
+  const uint8_t* p;
+  int64_t n;        // readable bytes of the stream
+  int64_t base;     // stream offset of window[0]
+  uint8_t* lds;     // kWin bytes (16-byte aligned)
+
+  __device__ void fill(int64_t at) {
+    // align the window to 16 bytes of absolute address so each lane moves one
+    // dwordx4; window covers [base, base + kWin) with base in (at - 16, at].
+    uintptr_t abs = (uintptr_t)(p + at);
+    uintptr_t ab = abs & ~(uintptr_t)15;
+    base = at - (int64_t)(abs - ab);
+    int l = lane_id();
+    int64_t off = base + l * 16;
+    uint4 v;
+    if (off >= 0 && off + 16 <= n) {
+      v = *(const uint4*)(p + off);
+    } else {
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (int k = 0; k < 16; k++) {
+        int64_t j = off + k;
+        if (j >= 0 && j < n) w[k >> 2] |= (uint32_t)p[j] << (8 * (k & 3));
+      }
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    *(uint4*)(lds + l * 16) = v;
+    __builtin_amdgcn_wave_barrier();
+  }
+  // byte at stream offset i, or -1 past the end
+  __device__ __forceinline__ int get(int64_t i) {
+    if (i < 0 || i >= n) return -1;
+    if (i < base || i >= base + kWin) fill(i);
+    return lds[i - base];
+  }
+};
+
+}  // namespace pqg

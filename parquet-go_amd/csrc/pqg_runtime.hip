@@ -1,0 +1,450 @@
+// pqg_runtime.hip — host runtime behind include/pqgpu.h (libpqgpu.so).
+//
+// One pqg_ctx per GPU: a HIP stream, grow-only device arenas and a pinned
+// host mirror of the job table.  pqg_decode_chunks_async enqueues the kernel
+// pipeline of pqg_kernels.hip for a batch of column chunks whose bytes are
+// already resident in HBM; pqg_sync waits and reports per-chunk status.  No
+// allocation or host synchronisation happens inside the enqueue once the
+// arenas have grown to the working-set size (capture-safe steady state).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/pqgpu.h"
+#include "pqg_common.h"
+
+namespace pqg {
+__global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs);
+__global__ void k_page_list(JobDev* jobs, int n_jobs, int* list, int list_cap, int* total, int* queues);
+__global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                         uint8_t* scratch);
+__global__ void k_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                         uint8_t* scratch, uint8_t* def_arena, uint8_t* rep_arena);
+__global__ void k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch);
+__global__ void k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                         uint8_t* value_arena);
+__global__ void k_finalize(JobDev* jobs, int n_jobs, PageDev* pages);
+}  // namespace pqg
+
+using namespace pqg;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int grow(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max(bytes, (size_t)256);
+    want = (want + 0xFFFFF) & ~(size_t)0xFFFFF;  // 1 MiB granules
+    if (hipMalloc(&p, want) != hipSuccess) {
+      p = nullptr;
+      return -1;
+    }
+    cap = want;
+    return 0;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+constexpr int kStages = 7;
+const char* kStageNames[kStages] = {"scan", "list", "snappy", "levels", "nn_scan", "values", "finalize"};
+
+int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+int value_width_of(const pqg_column_desc& c) {
+  switch (c.physical_type) {
+    case PQG_BOOLEAN: return 1;
+    case PQG_INT32: case PQG_FLOAT: return 4;
+    case PQG_INT64: case PQG_DOUBLE: return 8;
+    case PQG_INT96: return 12;
+    case PQG_FIXED_LEN_BYTE_ARRAY: return c.type_length > 0 ? c.type_length : 0;
+  }
+  return 0;
+}
+
+}  // namespace
+
+struct pqg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int num_cus = 256;
+  DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
+  JobDev* h_jobs = nullptr;  // pinned
+  int h_jobs_cap = 0;
+  std::vector<pqg_chunk_job> cur;       // jobs of the in-flight batch
+  std::vector<JobDev> plan;             // per-job capacities used
+  std::vector<int64_t> force_pages, force_slots, force_scratch, force_values;
+  int n_jobs = 0;
+  int64_t list_cap = 0;
+  hipEvent_t ev[kStages + 1];
+  bool timed = true;
+};
+
+static int hip_ok(hipError_t e) { return e == hipSuccess ? PQG_OK : PQG_ERR_HIP; }
+
+extern "C" {
+
+const char* pqg_status_string(int s) {
+  switch (s) {
+    case PQG_OK: return "ok";
+    case PQG_ERR_EOF: return "unexpected end of stream";
+    case PQG_ERR_THRIFT: return "page header: thrift decode failed";
+    case PQG_ERR_PAGE_HEADER: return "page header: missing or negative field";
+    case PQG_ERR_SIZE: return "page size mismatch";
+    case PQG_ERR_SNAPPY: return "snappy: corrupt input";
+    case PQG_ERR_RLE: return "rle: invalid run";
+    case PQG_ERR_DICT_INDEX: return "dict: invalid index";
+    case PQG_ERR_BIT_WIDTH: return "invalid bit width";
+    case PQG_ERR_DELTA: return "delta: invalid stream";
+    case PQG_ERR_UNSUPPORTED: return "unsupported encoding/codec/type";
+    case PQG_ERR_DICT_PAGE: return "there should be only one dictionary";
+    case PQG_ERR_BYTE_ARRAY: return "bytearray/plain: len is negative";
+    case PQG_ERR_LEVELS: return "level reader is not initialized";
+    case PQG_ERR_CAPACITY: return "capacity";
+    case PQG_ERR_INVALID_ARG: return "invalid argument";
+    case PQG_ERR_HIP: return "HIP runtime error";
+    case PQG_ERR_METADATA: return "invalid file metadata";
+  }
+  return "unknown";
+}
+
+int pqg_ctx_create(int device, pqg_ctx** out) {
+  if (!out) return PQG_ERR_INVALID_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return PQG_ERR_HIP;
+  if (hipSetDevice(device) != hipSuccess) return PQG_ERR_HIP;
+  pqg_ctx* c = new pqg_ctx();
+  c->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return PQG_ERR_HIP;
+  }
+  for (auto& e : c->ev) hipEventCreate(&e);
+  c->counters.grow(4096);
+  *out = c;
+  return PQG_OK;
+}
+
+void pqg_ctx_destroy(pqg_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  for (auto& e : c->ev) hipEventDestroy(e);
+  for (DevBuf* b : {&c->jobs, &c->pages, &c->list, &c->counters, &c->def_arena, &c->rep_arena, &c->value_arena,
+                    &c->scratch})
+    b->release();
+  if (c->h_jobs) hipHostFree(c->h_jobs);
+  hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int pqg_device_alloc(pqg_ctx* c, int64_t bytes, void** dptr) {
+  if (!c || !dptr) return PQG_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  return hip_ok(hipMalloc(dptr, (size_t)std::max<int64_t>(bytes, 1)));
+}
+int pqg_device_free(pqg_ctx* c, void* dptr) {
+  if (!c) return PQG_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  return hip_ok(hipFree(dptr));
+}
+int pqg_memcpy_h2d(pqg_ctx* c, void* dst, const void* src, int64_t bytes) {
+  if (!c) return PQG_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  int e = hip_ok(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, c->stream));
+  if (e) return e;
+  return hip_ok(hipStreamSynchronize(c->stream));
+}
+int pqg_memcpy_d2h(pqg_ctx* c, void* dst, const void* src, int64_t bytes) {
+  if (!c) return PQG_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  int e = hip_ok(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, c->stream));
+  if (e) return e;
+  return hip_ok(hipStreamSynchronize(c->stream));
+}
+
+// Plan arena regions for the current batch and upload the job table.
+static int plan_batch(pqg_ctx* c) {
+  const int n = c->n_jobs;
+  if (c->h_jobs_cap < n) {
+    if (c->h_jobs) hipHostFree(c->h_jobs);
+    c->h_jobs_cap = std::max(n, 64);
+    if (hipHostMalloc((void**)&c->h_jobs, sizeof(JobDev) * (size_t)c->h_jobs_cap) != hipSuccess) return PQG_ERR_HIP;
+  }
+  int64_t page_total = 0, slot_total = 0, value_total = 0, scratch_total = 0;
+  c->plan.resize((size_t)n);
+  for (int i = 0; i < n; i++) {
+    const pqg_chunk_job& in = c->cur[(size_t)i];
+    JobDev d;
+    memset(&d, 0, sizeof(d));
+    d.data = in.data;
+    d.data_len = in.data_len;
+    d.tcs = in.total_compressed_size;
+    d.data_page_offset = in.data_page_offset;
+    d.type = in.col.physical_type;
+    d.type_length = in.col.type_length;
+    d.max_def = in.col.max_def;
+    d.max_rep = in.col.max_rep;
+    d.codec = in.col.codec;
+    d.has_dict_off = in.has_dict_page_offset;
+    d.value_width = value_width_of(in.col);
+    int64_t pcap = in.total_compressed_size / 256 + 16;
+    if (c->force_pages[(size_t)i] > 0) pcap = c->force_pages[(size_t)i];
+    pcap = std::min<int64_t>(pcap, (int64_t)1 << 30);
+    d.page_cap = (int32_t)pcap;
+    d.page_base = page_total;
+    page_total += pcap;
+    int64_t scap = std::max<int64_t>(in.num_values_hint, 0) + 64;
+    if (c->force_slots[(size_t)i] > 0) scap = c->force_slots[(size_t)i];
+    d.slot_cap = scap;
+    d.slot_base = slot_total;
+    slot_total += align_up(scap, 256);
+    int64_t vcap = d.value_width > 0 ? scap * d.value_width : 0;
+    if (c->force_values[(size_t)i] > 0) vcap = c->force_values[(size_t)i];
+    d.value_cap = vcap;
+    d.value_base = value_total;
+    value_total += align_up(vcap, 256);
+    int64_t xcap = 0;
+    if (in.col.codec != PQG_CODEC_UNCOMPRESSED)
+      xcap = std::max<int64_t>(in.total_uncompressed_size, in.total_compressed_size) + pcap * 16 + 1024;
+    if (c->force_scratch[(size_t)i] > 0) xcap = c->force_scratch[(size_t)i];
+    d.scratch_cap = xcap;
+    d.scratch_base = scratch_total;
+    scratch_total += align_up(xcap, 256);
+    d.dict_page = -1;
+    d.error_page = -1;
+    c->plan[(size_t)i] = d;
+    c->h_jobs[i] = d;
+  }
+  c->list_cap = page_total;
+  if (c->jobs.grow(sizeof(JobDev) * (size_t)n) || c->pages.grow(sizeof(PageDev) * (size_t)page_total) ||
+      c->list.grow(sizeof(int) * (size_t)std::max<int64_t>(page_total, 1)) || c->def_arena.grow((size_t)slot_total + 64) ||
+      c->rep_arena.grow((size_t)slot_total + 64) || c->value_arena.grow((size_t)value_total + 64) ||
+      c->scratch.grow((size_t)scratch_total + 64))
+    return PQG_ERR_HIP;
+  return hip_ok(hipMemcpyAsync(c->jobs.p, c->h_jobs, sizeof(JobDev) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+}
+
+static int launch_pipeline(pqg_ctx* c) {
+  const int n = c->n_jobs;
+  JobDev* jobs = (JobDev*)c->jobs.p;
+  PageDev* pages = (PageDev*)c->pages.p;
+  int* list = (int*)c->list.p;
+  int* ctr = (int*)c->counters.p;  // [0] total pages, [8..15] queues
+  uint8_t* scratch = (uint8_t*)c->scratch.p;
+  const int waves = c->num_cus * 8;
+  hipStream_t s = c->stream;
+  if (c->timed) hipEventRecord(c->ev[0], s);
+  hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n);
+  if (c->timed) hipEventRecord(c->ev[1], s);
+  hipLaunchKernelGGL(k_page_list, dim3(1), dim3(256), 0, s, jobs, n, list, (int)std::min<int64_t>(c->list_cap, INT32_MAX),
+                     ctr, ctr + 8);
+  if (c->timed) hipEventRecord(c->ev[2], s);
+  bool any_comp = false;
+  for (int i = 0; i < n; i++) any_comp |= c->cur[(size_t)i].col.codec != PQG_CODEC_UNCOMPRESSED;
+  if (any_comp)
+    hipLaunchKernelGGL(k_snappy, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 8, scratch);
+  if (c->timed) hipEventRecord(c->ev[3], s);
+  hipLaunchKernelGGL(k_levels, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 9, scratch,
+                     (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p);
+  if (c->timed) hipEventRecord(c->ev[4], s);
+  hipLaunchKernelGGL(k_nn_scan, dim3(n), dim3(256), 0, s, jobs, pages, scratch);
+  if (c->timed) hipEventRecord(c->ev[5], s);
+  hipLaunchKernelGGL(k_values, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 10,
+                     (uint8_t*)c->value_arena.p);
+  if (c->timed) hipEventRecord(c->ev[6], s);
+  hipLaunchKernelGGL(k_finalize, dim3((n + 255) / 256), dim3(256), 0, s, jobs, n, pages);
+  if (c->timed) hipEventRecord(c->ev[7], s);
+  return hip_ok(hipGetLastError());
+}
+
+int pqg_decode_chunks_async(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs) {
+  if (!c || (!jobs && n_jobs) || n_jobs < 0) return PQG_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  for (int i = 0; i < n_jobs; i++) {
+    const pqg_column_desc& d = jobs[i].col;
+    if (d.max_def < 0 || d.max_def > 255 || d.max_rep < 0 || d.max_rep > 255) return PQG_ERR_INVALID_ARG;
+    if (jobs[i].data_len < 0 || jobs[i].total_compressed_size < 0 || (!jobs[i].data && jobs[i].data_len > 0))
+      return PQG_ERR_INVALID_ARG;
+  }
+  c->cur.assign(jobs, jobs + n_jobs);
+  c->n_jobs = n_jobs;
+  c->force_pages.assign((size_t)n_jobs, 0);
+  c->force_slots.assign((size_t)n_jobs, 0);
+  c->force_scratch.assign((size_t)n_jobs, 0);
+  c->force_values.assign((size_t)n_jobs, 0);
+  if (n_jobs == 0) return PQG_OK;
+  int e = plan_batch(c);
+  if (e) return e;
+  return launch_pipeline(c);
+}
+
+// Copy job results back; grow and re-run chunks that ran out of arena space.
+int pqg_sync(pqg_ctx* c, pqg_chunk_result* results, int n_jobs) {
+  if (!c || n_jobs != c->n_jobs) return PQG_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  const int n = c->n_jobs;
+  if (n == 0) return PQG_OK;
+  for (int attempt = 0; attempt < 3; attempt++) {
+    if (hipMemcpyAsync(c->h_jobs, c->jobs.p, sizeof(JobDev) * (size_t)n, hipMemcpyDeviceToHost, c->stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+      return PQG_ERR_HIP;
+    bool retry = false;
+    for (int i = 0; i < n; i++) {
+      const JobDev& d = c->h_jobs[i];
+      if (d.status != PQG_ERR_CAPACITY) continue;
+      retry = true;
+      c->force_pages[(size_t)i] = std::max<int64_t>((int64_t)d.num_pages + 16, d.page_cap);
+      c->force_slots[(size_t)i] = std::max<int64_t>(d.num_slots + 64, d.slot_cap);
+      c->force_scratch[(size_t)i] = std::max<int64_t>(d.need_scratch + 1024, d.scratch_cap);
+      int64_t nv = std::max<int64_t>(d.num_values, d.num_slots);
+      c->force_values[(size_t)i] = std::max<int64_t>(nv * std::max(d.value_width, 1) + 64, d.value_cap);
+    }
+    if (!retry) break;
+    int e = plan_batch(c);
+    if (e) return e;
+    e = launch_pipeline(c);
+    if (e) return e;
+  }
+  for (int i = 0; i < n; i++) {
+    const JobDev& d = c->h_jobs[i];
+    pqg_chunk_result& r = results[i];
+    memset(&r, 0, sizeof(r));
+    r.status = d.status;
+    r.error_page = d.error_page;
+    r.num_pages = d.status == PQG_ERR_CAPACITY ? 0 : d.n_out_pages;
+    r.value_width = d.value_width;
+    r.num_slots = d.num_slots;
+    r.num_values = d.num_values;
+    r.values_bytes = d.values_bytes;
+    r.def_levels = d.max_def > 0 ? (uint8_t*)c->def_arena.p + d.slot_base : nullptr;
+    r.rep_levels = d.max_rep > 0 ? (uint8_t*)c->rep_arena.p + d.slot_base : nullptr;
+    r.values = (uint8_t*)c->value_arena.p + d.value_base;
+    r.offsets = nullptr;
+  }
+  return PQG_OK;
+}
+
+int pqg_decode_chunks(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs, pqg_chunk_result* results) {
+  int e = pqg_decode_chunks_async(c, jobs, n_jobs);
+  if (e) return e;
+  return pqg_sync(c, results, n_jobs);
+}
+
+int pqg_get_pages(pqg_ctx* c, int job, pqg_page_info* out, int cap) {
+  if (!c || job < 0 || job >= c->n_jobs) return PQG_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  const JobDev& d = c->h_jobs[job];
+  int np = std::min<int>(d.n_out_pages, d.page_cap);
+  if (d.status == PQG_ERR_CAPACITY) np = 0;
+  std::vector<PageDev> tmp((size_t)np);
+  if (np > 0) {
+    if (hipMemcpyAsync(tmp.data(), (PageDev*)c->pages.p + d.page_base, sizeof(PageDev) * (size_t)np,
+                       hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+      return PQG_ERR_HIP;
+  }
+  int k = 0;
+  for (int i = 0; i < np && i < cap; i++, k++) {
+    const PageDev& p = tmp[(size_t)i];
+    pqg_page_info& o = out[i];
+    memset(&o, 0, sizeof(o));
+    o.header_offset = p.header_offset;
+    o.payload_offset = p.payload_offset;
+    o.slot_offset = p.slot_offset;
+    o.value_offset = p.value_offset;
+    o.page_type = p.page_type;
+    o.encoding = p.encoding;
+    o.num_values = p.num_values;
+    o.not_null = p.not_null;
+    o.compressed_size = p.csize;
+    o.uncompressed_size = p.usize;
+    o.def_len = p.def_len;
+    o.rep_len = p.rep_len;
+    o.def_encoding = p.def_enc;
+    o.rep_encoding = p.rep_enc;
+    o.status = p.read_status != PQG_OK ? p.read_status : p.decode_status;
+    o.flags = p.flags;
+  }
+  return k;
+}
+
+int pqg_last_timings(pqg_ctx* c, float* out, int cap) {
+  if (!c || !out) return PQG_ERR_INVALID_ARG;
+  int k = 0;
+  float tot = 0;
+  hipEventElapsedTime(&tot, c->ev[0], c->ev[kStages]);
+  if (k < cap) out[k++] = tot;
+  for (int i = 0; i < kStages && k < cap; i++) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]);
+    out[k++] = ms;
+  }
+  return k;
+}
+
+int pqg_bench_decode(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs, int iters, float* ms_total, float* ms_stage,
+                     int stage_cap) {
+  if (!c || iters < 1) return PQG_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  std::vector<pqg_chunk_result> res((size_t)std::max(n_jobs, 1));
+  // first call sizes the arenas (and retries on capacity)
+  int e = pqg_decode_chunks(c, jobs, n_jobs, res.data());
+  if (e) return e;
+  // freeze the capacities found by the first call
+  std::vector<int64_t> fp(c->force_pages), fs(c->force_slots), fx(c->force_scratch), fv(c->force_values);
+  for (int i = 0; i < n_jobs; i++) {
+    fp[(size_t)i] = c->h_jobs[i].page_cap;
+    fs[(size_t)i] = c->h_jobs[i].slot_cap;
+    fx[(size_t)i] = c->h_jobs[i].scratch_cap;
+    fv[(size_t)i] = c->h_jobs[i].value_cap;
+  }
+  c->force_pages = fp;
+  c->force_slots = fs;
+  c->force_scratch = fx;
+  c->force_values = fv;
+  e = plan_batch(c);
+  if (e) return e;
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  std::vector<float> stage_acc(kStages, 0.f);
+  hipEventRecord(a, c->stream);
+  for (int it = 0; it < iters; it++) {
+    e = launch_pipeline(c);
+    if (e) break;
+  }
+  hipEventRecord(b, c->stream);
+  hipStreamSynchronize(c->stream);
+  float ms = 0;
+  hipEventElapsedTime(&ms, a, b);
+  if (ms_total) *ms_total = ms / (float)iters;
+  if (ms_stage) {
+    for (int i = 0; i < kStages && i < stage_cap; i++) {
+      float x = 0;
+      hipEventElapsedTime(&x, c->ev[i], c->ev[i + 1]);
+      ms_stage[i] = x;
+    }
+  }
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  return e;
+}
+
+}  // extern "C"

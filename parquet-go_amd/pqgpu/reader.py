@@ -1,0 +1,214 @@
+"""Host-side mirror of parquet-go's reader surface over libpqgpu.
+
+parquet-go (fraugster/parquet-go v0.2.1) reads a file with
+    NewFileReader(r, columns...)      file_reader.go:27-48
+    FileReader.readRowGroup / PreLoad file_reader.go:51-98  → readRowGroup chunk_reader.go:404-431
+and decodes each selected column chunk with readChunk → readPages →
+readPageData (chunk_reader.go:206-402).  This module keeps those names and
+meanings; the page decode itself runs in the HIP kernels of libpqgpu.
+Column projection follows schema.isSelected (schema.go:296-312): an empty
+selection reads every column.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from ._lib import lib
+
+
+class PqgError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = int(code)
+        super().__init__("%s: %s (%d)" % (what, abi.status_name(code), code))
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise PqgError(rc, what)
+
+
+class ParquetFile:
+    """Footer + schema of a file held in host memory (readFileMetaData file_meta.go:14-62)."""
+
+    def __init__(self, data):
+        self.data = bytes(data)
+        self._buf = np.frombuffer(self.data, dtype=np.uint8)
+        h = C.c_void_p()
+        _check(lib().pqg_file_open(self.data, len(self.data), C.byref(h)), "pqg_file_open")
+        self._h = h
+        L = lib()
+        self.num_columns = L.pqg_file_num_columns(h)
+        self.num_row_groups = L.pqg_file_num_row_groups(h)
+        self.num_rows = L.pqg_file_num_rows(h)
+        self.columns = []
+        for i in range(self.num_columns):
+            ci = abi.ColumnInfo()
+            _check(L.pqg_file_column(h, i, C.byref(ci)), "pqg_file_column")
+            self.columns.append(ci)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().pqg_file_close(h)
+            self._h = None
+
+    def column_index(self, path):
+        for i, c in enumerate(self.columns):
+            if c.path.decode() == path:
+                return i
+        raise KeyError(path)
+
+    def row_group_rows(self, rg):
+        return lib().pqg_file_row_group_rows(self._h, rg)
+
+    def chunk_meta(self, rg, col):
+        m = abi.ChunkMeta()
+        _check(lib().pqg_file_chunk(self._h, rg, col, C.byref(m)), "pqg_file_chunk")
+        return m
+
+    def host_job(self, rg, col):
+        """A chunk job whose data pointer is HOST memory (for the CPU oracle)."""
+        m = self.chunk_meta(rg, col)
+        job = abi.ChunkJob()
+        job.col = self.columns[col].desc
+        job.col.codec = m.codec
+        start = max(0, min(m.start, len(self.data)))
+        job.data = self._buf.ctypes.data + start
+        job.data_len = len(self.data) - start
+        job.total_compressed_size = m.total_compressed_size
+        job.data_page_offset = m.data_page_offset - m.start
+        job.num_values_hint = m.num_values
+        job.total_uncompressed_size = m.total_uncompressed_size
+        job.has_dict_page_offset = m.has_dict_page_offset
+        return job, m
+
+
+class DecodedColumn:
+    """Decoded chunk on the host: def/rep levels + dense values[:nn] (readValues outputs)."""
+
+    def __init__(self, status, error_page, num_slots, num_values, value_width, def_levels, rep_levels, values,
+                 pages):
+        self.status = status
+        self.error_page = error_page
+        self.num_slots = num_slots
+        self.num_values = num_values
+        self.value_width = value_width
+        self.def_levels = def_levels
+        self.rep_levels = rep_levels
+        self.values = values
+        self.pages = pages
+
+
+class GpuDecoder:
+    """One decode context per GPU (pqg_ctx)."""
+
+    def __init__(self, device=0):
+        self.L = lib()
+        h = C.c_void_p()
+        _check(self.L.pqg_ctx_create(device, C.byref(h)), "pqg_ctx_create")
+        self.ctx = h
+        self._bufs = []
+
+    def close(self):
+        for p in self._bufs:
+            self.L.pqg_device_free(self.ctx, p)
+        self._bufs = []
+        if self.ctx:
+            self.L.pqg_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- device memory
+    def upload(self, data):
+        arr = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        p = C.c_void_p()
+        _check(self.L.pqg_device_alloc(self.ctx, max(arr.nbytes, 1), C.byref(p)), "pqg_device_alloc")
+        if arr.nbytes:
+            _check(self.L.pqg_memcpy_h2d(self.ctx, p, arr.ctypes.data, arr.nbytes), "pqg_memcpy_h2d")
+        self._bufs.append(p)
+        return p.value
+
+    def free(self, ptr):
+        for i, p in enumerate(self._bufs):
+            if p.value == ptr:
+                self.L.pqg_device_free(self.ctx, p)
+                del self._bufs[i]
+                return
+
+    def d2h(self, ptr, nbytes, dtype=np.uint8):
+        out = np.empty(max(nbytes, 0), dtype=np.uint8)
+        if nbytes > 0:
+            _check(self.L.pqg_memcpy_d2h(self.ctx, out.ctypes.data, C.c_void_p(ptr), nbytes), "pqg_memcpy_d2h")
+        return out.view(dtype) if dtype != np.uint8 else out
+
+    # ---- decode
+    def decode_jobs(self, jobs):
+        n = len(jobs)
+        arr = (abi.ChunkJob * max(n, 1))(*jobs)
+        res = (abi.ChunkResult * max(n, 1))()
+        _check(self.L.pqg_decode_chunks(self.ctx, arr, n, res), "pqg_decode_chunks")
+        return [res[i] for i in range(n)]
+
+    def pages(self, job_index, cap=1 << 20):
+        buf = (abi.PageInfo * cap)()
+        k = self.L.pqg_get_pages(self.ctx, job_index, buf, cap)
+        if k < 0:
+            raise PqgError(k, "pqg_get_pages")
+        return [buf[i] for i in range(k)]
+
+    def timings(self):
+        out = (C.c_float * 16)()
+        k = self.L.pqg_last_timings(self.ctx, out, 16)
+        return [out[i] for i in range(max(k, 0))]
+
+    def download(self, r, job_index=None):
+        lv_def = self.d2h(r.def_levels, r.num_slots) if (r.def_levels and r.status == 0) else None
+        lv_rep = self.d2h(r.rep_levels, r.num_slots) if (r.rep_levels and r.status == 0) else None
+        vals = self.d2h(r.values, r.values_bytes) if r.status == 0 else None
+        pages = self.pages(job_index) if job_index is not None else None
+        return DecodedColumn(r.status, r.error_page, r.num_slots, r.num_values, r.value_width, lv_def, lv_rep,
+                             vals, pages)
+
+
+def device_job(pf: ParquetFile, rg, col, dev_ptr_of_file):
+    """Chunk job pointing into a device copy of the whole file."""
+    job, m = pf.host_job(rg, col)
+    start = max(0, min(m.start, len(pf.data)))
+    job.data = dev_ptr_of_file + start
+    return job
+
+
+class FileReader:
+    """Mirror of parquet-go's FileReader (file_reader.go): selected columns of a
+    file, decoded one row group at a time on the GPU."""
+
+    def __init__(self, data, *columns, device=0, decoder=None):
+        self.file = ParquetFile(data)
+        self.dec = decoder or GpuDecoder(device)
+        self._dev = self.dec.upload(self.file.data)
+        self.selected = [self.file.column_index(c) for c in columns] if columns else list(range(self.file.num_columns))
+        self.row_group_position = 0
+
+    def row_group_count(self):
+        return self.file.num_row_groups
+
+    def num_rows(self):
+        return self.file.num_rows
+
+    def read_row_group(self, rg):
+        """readRowGroup (chunk_reader.go:404-431) for the selected columns."""
+        jobs = [device_job(self.file, rg, c, self._dev) for c in self.selected]
+        res = self.dec.decode_jobs(jobs)
+        out = {}
+        for i, (c, r) in enumerate(zip(self.selected, res)):
+            out[self.file.columns[c].path.decode()] = self.dec.download(r, i)
+        return out
+
+    def close(self):
+        self.dec.free(self._dev)

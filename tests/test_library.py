@@ -1,0 +1,65 @@
+"""CPU-side checks of the product library: it loads, exports every symbol the
+C ABI header declares, and its host planner (footer + schema) works."""
+import os
+import re
+
+import numpy as np
+
+import pqgpu
+from gen import pqwrite as W
+from pqgpu import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols(prefix):
+    text = open(os.path.join(ROOT, "include", "pqgpu.h")).read()
+    return sorted(set(re.findall(r"\b(%s_[a-z0-9_]+)\s*\(" % prefix, text)))
+
+
+def test_library_exports_header_symbols():
+    L = _lib.lib()
+    syms = header_symbols("pqg")
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(_lib.EXPORTED) == sorted(syms)
+
+
+def test_oracle_exports_header_symbols():
+    from oracle import pyoracle
+    L = pyoracle.lib()
+    for s in header_symbols("pqo"):
+        assert hasattr(L, s), s
+
+
+def test_product_does_not_link_oracle():
+    import subprocess
+    out = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in out
+    nm = subprocess.run(["nm", "-D", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "pqo_" not in nm
+
+
+def test_planner_schema_levels():
+    rng = np.random.default_rng(1)
+    n = 1000
+    cols = [W.Column("req", W.INT64, rng.integers(0, 9, n)),
+            W.Column("opt", W.INT32, rng.integers(0, 9, n).astype(np.int32)[: n - 10], repetition=W.OPTIONAL,
+                     def_levels=np.r_[np.ones(n - 10), np.zeros(10)].astype(np.uint8)),
+            W.Column("lst", W.DOUBLE, np.arange(n, dtype=np.float64), repetition=W.LIST,
+                     def_levels=np.full(n, 3), rep_levels=np.zeros(n))]
+    data = W.write_file(cols, n, row_groups=3)
+    pf = pqgpu.ParquetFile(data)
+    assert pf.num_columns == 3 and pf.num_row_groups == 3 and pf.num_rows == n
+    d = [(c.path.decode(), c.desc.max_def, c.desc.max_rep) for c in pf.columns]
+    assert d == [("req", 0, 0), ("opt", 1, 0), ("lst.list.element", 3, 1)]
+    m = pf.chunk_meta(1, 2)
+    assert m.total_compressed_size > 0 and m.num_values == 334
+
+
+def test_planner_rejects_bad_footer():
+    import pytest
+    for bad in (b"", b"PAR1", b"PAR1xxxxPAR1", b"PAR1" + b"\x00" * 8 + b"\xff\xff\xff\x7fPAR1"):
+        with pytest.raises(pqgpu.PqgError):
+            pqgpu.ParquetFile(bad)
