@@ -212,6 +212,12 @@ int pqg_last_timings(pqg_ctx* ctx, float* out, int cap);
 int pqg_bench_decode(pqg_ctx* ctx, const pqg_chunk_job* jobs, int n_jobs, int iters,
                      float* ms_total, float* ms_stage, int stage_cap);
 
+/* Diagnostics of the last decode for job `job` (after pqg_sync): out[0] = 1
+ * when its page list came from the serial header walk (K1e) instead of the
+ * speculative parallel scan, out[1] = header candidates found, out[2] =
+ * pages, out[3] = decompressed scratch bytes.  Returns entries written. */
+int pqg_debug_job(pqg_ctx* ctx, int job, int64_t* out, int cap);
+
 /* ---- host-side planner: footer / schema (file_meta.go:14-62, schema.go) --- */
 typedef struct pqg_file pqg_file;
 

@@ -36,6 +36,7 @@ enum : int32_t {
   kBYTE_ARRAY = -12,
   kLEVELS = -13,
   kCAPACITY = -20,
+  kCOMPLEX = -30,   // internal: header needs the serial walk (deep thrift nesting)
 };
 
 // Header fields of one page (thrift PageHeader subset, parquet.go:5794-5803).
@@ -95,6 +96,32 @@ struct JobDev {
   int64_t dict_count, dict_len;
   const int64_t* dict_offs;  // variable-length dictionary offsets (count+1)
   int32_t flags, pad;
+  // ---- K1 speculative page scan (see k_page_cands / k_page_chain)
+  int64_t tile_base;       // first scan tile of this job (global tile index)
+  int32_t n_tiles;         // ceil(min(tcs, data_len) / kScanTile)
+  int32_t scan_fallback;   // 1: the serial walk (k_scan_pages) decodes this job's page list
+  int32_t n_cands;         // header candidates found in the job's bytes
+  int32_t n_ok;            // candidates whose read phase succeeds
+  int32_t brk;             // first ok-rank whose successor is not the next ok candidate
+  int32_t first_dict;      // first ok-rank of a dictionary page
+};
+
+// Scan tiles of the speculative page-header search.
+constexpr int kScanTile = 16384;
+constexpr int kCandPerTile = 64;
+
+// A page-header candidate: a position whose bytes parse as a PageHeader
+// (parsed by one lane, classified as if it were the chunk's first dictionary
+// page when it is one).  The chain kernel keeps the ones reachable from
+// position 0 by next-page links.
+struct Cand {
+  int64_t pos, next, payload;
+  int64_t comp;            // scratch bytes of its decompressed block (16-rounded), 0 if none
+  int32_t type, encoding, num_values, csize, usize;
+  int32_t def_len, rep_len, def_enc, rep_enc;
+  int32_t status;          // read-phase status, kCOMPLEX: re-parse serially
+  int32_t okrank;          // rank among the tile's candidates with status kOK
+  int32_t pad;
 };
 
 }  // namespace pqg

@@ -94,6 +94,30 @@ __device__ __forceinline__ int64_t wave_excl_scan_i64(int64_t v, int64_t* total)
   return x - v;
 }
 
+// Block-wide exclusive scan (NT threads, NT/64 waves); `part` holds NT/64+1
+// entries of LDS.  Every thread of the block must call it.
+template <int NT>
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* total, int64_t* part) {
+  constexpr int NW = NT / 64;
+  const int lane = lane_id(), wid = (int)(threadIdx.x >> 6);
+  int64_t wt;
+  const int64_t ex = wave_excl_scan_i64(v, &wt);
+  if (lane == 0) part[wid] = wt;
+  __syncthreads();
+  if (wid == 0) {
+    int64_t x = lane < NW ? part[lane] : 0, t;
+    int64_t e = wave_excl_scan_i64(x, &t);
+    __builtin_amdgcn_wave_barrier();
+    if (lane < NW) part[lane] = e;
+    if (lane == 0) part[NW] = t;
+  }
+  __syncthreads();
+  const int64_t r = ex + part[wid];
+  *total = part[NW];
+  __syncthreads();
+  return r;
+}
+
 // ---------------------------------------------------------------------------
 // LDS byte window over a device stream, refilled cooperatively by the wave.
 // All lanes call get() with the same position (wave-uniform control flow).

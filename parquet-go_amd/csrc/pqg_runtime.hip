@@ -18,6 +18,13 @@
 #include "pqg_common.h"
 
 namespace pqg {
+__global__ void k_page_cands(JobDev* jobs, int n_jobs, int* tile_count, int* tile_okc, Cand* cands);
+__global__ void k_tile_scan(JobDev* jobs, const int* tile_count, const int* tile_okc, int* tile_off, int* tile_okoff);
+__global__ void k_cand_link(JobDev* jobs, int n_jobs, int64_t total_tiles, const int* tile_count,
+                            const int* tile_off, const int* tile_okoff, const Cand* cands, int* succ, int* idx2slot,
+                            int* ok2slot);
+__global__ void k_page_chain(JobDev* jobs, PageDev* pages, const Cand* cands, const int* succ,
+                             const int* idx2slot, const int* ok2slot, int* order);
 __global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs);
 __global__ void k_page_list(JobDev* jobs, int n_jobs, int* list, int list_cap, int* total, int* queues);
 __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
@@ -59,7 +66,7 @@ struct DevBuf {
 };
 
 constexpr int kStages = 7;
-const char* kStageNames[kStages] = {"scan", "list", "snappy", "levels", "nn_scan", "values", "finalize"};
+// stages timed by pqg_last_timings: scan (K1a-e), list, snappy, levels, nn_scan, values, finalize
 
 int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
@@ -81,6 +88,8 @@ struct pqg_ctx {
   hipStream_t stream = nullptr;
   int num_cus = 256;
   DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
+  DevBuf tile_count, tile_okc, tile_off, tile_okoff, cands, succ, idx2slot, ok2slot, order;  // K1 page scan
+  int64_t total_tiles = 0;
   JobDev* h_jobs = nullptr;  // pinned
   int h_jobs_cap = 0;
   std::vector<pqg_chunk_job> cur;       // jobs of the in-flight batch
@@ -146,7 +155,8 @@ void pqg_ctx_destroy(pqg_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (auto& e : c->ev) hipEventDestroy(e);
   for (DevBuf* b : {&c->jobs, &c->pages, &c->list, &c->counters, &c->def_arena, &c->rep_arena, &c->value_arena,
-                    &c->scratch})
+                    &c->scratch, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cands, &c->succ, &c->idx2slot,
+                    &c->ok2slot, &c->order})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
   hipStreamDestroy(c->stream);
@@ -186,7 +196,7 @@ static int plan_batch(pqg_ctx* c) {
     c->h_jobs_cap = std::max(n, 64);
     if (hipHostMalloc((void**)&c->h_jobs, sizeof(JobDev) * (size_t)c->h_jobs_cap) != hipSuccess) return PQG_ERR_HIP;
   }
-  int64_t page_total = 0, slot_total = 0, value_total = 0, scratch_total = 0;
+  int64_t page_total = 0, slot_total = 0, value_total = 0, scratch_total = 0, tile_total = 0;
   c->plan.resize((size_t)n);
   for (int i = 0; i < n; i++) {
     const pqg_chunk_job& in = c->cur[(size_t)i];
@@ -228,6 +238,10 @@ static int plan_batch(pqg_ctx* c) {
     scratch_total += align_up(xcap, 256);
     d.dict_page = -1;
     d.error_page = -1;
+    const int64_t lim = std::max<int64_t>(0, std::min(in.total_compressed_size, in.data_len));
+    d.tile_base = tile_total;
+    d.n_tiles = (int32_t)((lim + kScanTile - 1) / kScanTile);
+    tile_total += d.n_tiles;
     c->plan[(size_t)i] = d;
     c->h_jobs[i] = d;
   }
@@ -235,8 +249,16 @@ static int plan_batch(pqg_ctx* c) {
   if (c->jobs.grow(sizeof(JobDev) * (size_t)n) || c->pages.grow(sizeof(PageDev) * (size_t)page_total) ||
       c->list.grow(sizeof(int) * (size_t)std::max<int64_t>(page_total, 1)) || c->def_arena.grow((size_t)slot_total + 64) ||
       c->rep_arena.grow((size_t)slot_total + 64) || c->value_arena.grow((size_t)value_total + 64) ||
-      c->scratch.grow((size_t)scratch_total + 64))
+      c->scratch.grow((size_t)scratch_total + 64) || c->tile_count.grow(sizeof(int) * (size_t)tile_total + 64) ||
+      c->tile_off.grow(sizeof(int) * (size_t)tile_total + 64) || c->tile_okc.grow(sizeof(int) * (size_t)tile_total + 64) ||
+      c->tile_okoff.grow(sizeof(int) * (size_t)tile_total + 64) ||
+      c->ok2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
+      c->cands.grow(sizeof(Cand) * (size_t)tile_total * kCandPerTile + 64) ||
+      c->succ.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
+      c->idx2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
+      c->order.grow(sizeof(int) * (size_t)page_total + 64))
     return PQG_ERR_HIP;
+  c->total_tiles = tile_total;
   return hip_ok(hipMemcpyAsync(c->jobs.p, c->h_jobs, sizeof(JobDev) * (size_t)n, hipMemcpyHostToDevice, c->stream));
 }
 
@@ -250,6 +272,19 @@ static int launch_pipeline(pqg_ctx* c) {
   const int waves = c->num_cus * 8;
   hipStream_t s = c->stream;
   if (c->timed) hipEventRecord(c->ev[0], s);
+  const int64_t nt = c->total_tiles;
+  int* tcount = (int*)c->tile_count.p;
+  int* toff = (int*)c->tile_off.p;
+  Cand* cands = (Cand*)c->cands.p;
+  int* tokc = (int*)c->tile_okc.p;
+  int* tokoff = (int*)c->tile_okoff.p;
+  if (nt > 0) hipLaunchKernelGGL(k_page_cands, dim3((unsigned)nt), dim3(256), 0, s, jobs, n, tcount, tokc, cands);
+  hipLaunchKernelGGL(k_tile_scan, dim3(n), dim3(1024), 0, s, jobs, tcount, tokc, toff, tokoff);
+  if (nt > 0)
+    hipLaunchKernelGGL(k_cand_link, dim3((unsigned)((nt * kCandPerTile + 255) / 256)), dim3(256), 0, s, jobs, n, nt,
+                       tcount, toff, tokoff, cands, (int*)c->succ.p, (int*)c->idx2slot.p, (int*)c->ok2slot.p);
+  hipLaunchKernelGGL(k_page_chain, dim3(n), dim3(1024), 0, s, jobs, pages, cands, (const int*)c->succ.p,
+                     (const int*)c->idx2slot.p, (const int*)c->ok2slot.p, (int*)c->order.p);
   hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n);
   if (c->timed) hipEventRecord(c->ev[1], s);
   hipLaunchKernelGGL(k_page_list, dim3(1), dim3(256), 0, s, jobs, n, list, (int)std::min<int64_t>(c->list_cap, INT32_MAX),
@@ -268,7 +303,7 @@ static int launch_pipeline(pqg_ctx* c) {
   hipLaunchKernelGGL(k_values, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 10,
                      (uint8_t*)c->value_arena.p);
   if (c->timed) hipEventRecord(c->ev[6], s);
-  hipLaunchKernelGGL(k_finalize, dim3((n + 255) / 256), dim3(256), 0, s, jobs, n, pages);
+  hipLaunchKernelGGL(k_finalize, dim3(n), dim3(256), 0, s, jobs, n, pages);
   if (c->timed) hipEventRecord(c->ev[7], s);
   return hip_ok(hipGetLastError());
 }
@@ -382,6 +417,15 @@ int pqg_get_pages(pqg_ctx* c, int job, pqg_page_info* out, int cap) {
     o.status = p.read_status != PQG_OK ? p.read_status : p.decode_status;
     o.flags = p.flags;
   }
+  return k;
+}
+
+int pqg_debug_job(pqg_ctx* c, int job, int64_t* out, int cap) {
+  if (!c || !out || job < 0 || job >= c->n_jobs) return PQG_ERR_INVALID_ARG;
+  const JobDev& d = c->h_jobs[job];
+  const int64_t v[4] = {d.scan_fallback, d.n_cands, d.num_pages, d.need_scratch};
+  int k = 0;
+  for (; k < 4 && k < cap; k++) out[k] = v[k];
   return k;
 }
 

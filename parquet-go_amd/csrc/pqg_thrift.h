@@ -42,6 +42,13 @@ struct Compact {
   int nlast;
   int16_t last_id;
   bool bool_set, bool_val;
+  // Stack capacities.  The serial walk uses the full kMax* limits (hitting
+  // them is a thrift error); the speculative per-lane candidate parse
+  // (k_page_cands) uses small stacks and reports `overflow` instead, so the
+  // page is re-parsed by the serial walk rather than misclassified.
+  int fcap = kMaxFrames;
+  int lcap = kMaxLast;
+  bool overflow = false;
 
   __host__ __device__ int byte(uint8_t* b) {
     int v = src.get(pos);
@@ -94,7 +101,10 @@ struct Compact {
     return -1;
   }
   __host__ __device__ int struct_begin() {
-    if (nlast >= kMaxLast) return -1;
+    if (nlast >= lcap) {
+      if (lcap < kMaxLast) overflow = true;
+      return -1;
+    }
     last[nlast++] = last_id;
     last_id = 0;
     return 0;
@@ -171,7 +181,7 @@ struct Compact {
         return 0;
       case T_STRING: return binary_skip();
       case T_STRUCT: {
-        if (*nf >= kMaxFrames) return -1;
+        if (*nf >= fcap) { if (fcap < kMaxFrames) overflow = true; return -1; }
         if (struct_begin()) return -1;
         SkipFrame& f = frames[(*nf)++];
         f.kind = T_STRUCT;
@@ -187,7 +197,7 @@ struct Compact {
         if (size < 0) return -1;
         uint8_t kv = 0;
         if (size != 0 && byte(&kv)) return -1;
-        if (*nf >= kMaxFrames) return -1;
+        if (*nf >= fcap) { if (fcap < kMaxFrames) overflow = true; return -1; }
         SkipFrame& f = frames[(*nf)++];
         f.kind = T_MAP;
         f.depth = (int8_t)depth;
@@ -210,7 +220,7 @@ struct Compact {
         }
         int et = ttype(st);
         if (et < 0) return -1;
-        if (*nf >= kMaxFrames) return -1;
+        if (*nf >= fcap) { if (fcap < kMaxFrames) overflow = true; return -1; }
         SkipFrame& f = frames[(*nf)++];
         f.kind = T_LIST;
         f.depth = (int8_t)depth;

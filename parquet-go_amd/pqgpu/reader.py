@@ -162,6 +162,14 @@ class GpuDecoder:
             raise PqgError(k, "pqg_get_pages")
         return [buf[i] for i in range(k)]
 
+    def debug_job(self, job_index):
+        """(serial_walk, candidates, pages, scratch_bytes) of the last decode."""
+        out = (C.c_int64 * 4)()
+        k = self.L.pqg_debug_job(self.ctx, job_index, out, 4)
+        if k < 0:
+            raise PqgError(k, "pqg_debug_job")
+        return tuple(int(out[i]) for i in range(k))
+
     def timings(self):
         out = (C.c_float * 16)()
         k = self.L.pqg_last_timings(self.ctx, out, 16)

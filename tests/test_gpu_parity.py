@@ -290,3 +290,78 @@ def test_fuzz_mutations(dec):
             P.compare_file(bytes(b), dec)
             n_cases += 1
     assert n_cases == 240
+
+
+def _decode_one(dec, data):
+    """Decode every chunk of `data` on the GPU, compare with the oracle, and
+    return the K1 diagnostics of job 0 (serial_walk, candidates, pages, scratch)."""
+    P.compare_file(data, dec)
+    return dec.debug_job(0)
+
+
+def test_scan_speculative_path_used(dec):
+    # ordinary multi-page chunks: the parallel candidate scan settles the page list
+    data, _ = W.config_c2(rows=200_000, bits=8, rows_per_page=20000)
+    walk, cands, pages, _ = _decode_one(dec, data)
+    assert walk == 0 and pages == 11 and cands >= pages
+    data, _ = W.config_c3(rows=100_000, rows_per_page=20000)
+    walk, cands, pages, scratch = _decode_one(dec, data)
+    assert walk == 0 and pages == 5 and scratch > 0
+
+
+def test_scan_false_candidates_are_skipped(dec):
+    # PLAIN int32 payload bytes 15 00 15 00 parse as page-header prefixes: a few
+    # per tile are false candidates the chain must jump over
+    n = 60_000
+    v = np.arange(n, dtype=np.int32)
+    v[::997] = 0x00150015
+    data = W.write_file([W.Column("x", W.INT32, v, rows_per_page=5000)], n)
+    walk, cands, pages, _ = _decode_one(dec, data)
+    assert walk == 0 and pages == 12 and cands > pages
+
+
+def test_scan_false_ok_headers_walked(dec):
+    # a complete, valid DataPageHeader embedded in PLAIN payload bytes: an ok
+    # false candidate between two real pages (the chain is walked around it)
+    fake = bytes([0x15, 0x00, 0x15, 0x02, 0x15, 0x02, 0x2C, 0x15, 0x02, 0x15, 0x00, 0x15, 0x00, 0x15, 0x00,
+                  0x00, 0x00, 0, 0, 0])
+    n = 60_000
+    v = np.arange(n, dtype=np.int32)
+    fk = np.frombuffer(fake, dtype=np.int32)
+    for at in range(1000, n - 10, 7919):
+        v[at:at + len(fk)] = fk
+    for codec in (W.UNCOMPRESSED, W.SNAPPY):
+        data = W.write_file([W.Column("x", W.INT32, v, rows_per_page=5000, codec=codec)], n)
+        walk, cands, pages, _ = _decode_one(dec, data)
+        assert walk == 0 and pages == 12
+
+
+def test_scan_tile_overflow_falls_back(dec):
+    # every value is a header prefix: > kCandPerTile hits per tile -> serial walk
+    n = 40_000
+    v = np.full(n, 0x00150015, dtype=np.int32)
+    data = W.write_file([W.Column("x", W.INT32, v, rows_per_page=9000)], n)
+    walk, _, pages, _ = _decode_one(dec, data)
+    assert walk == 1 and pages == 5
+
+
+def test_scan_tiny_pages(dec):
+    # many pages per 16 KiB tile (fallback or not, the page list must match)
+    n = 5000
+    v = np.arange(n, dtype=np.int64)
+    data = W.write_file([W.Column("x", W.INT64, v, rows_per_page=7)], n)
+    P.compare_file(data, dec)
+    data = W.write_file([W.Column("x", W.INT64, v, rows_per_page=300)], n)
+    walk, _, pages, _ = _decode_one(dec, data)
+    assert walk == 0 and pages == (n + 299) // 300
+
+
+def test_scan_garbage_lists_bounded(dec):
+    # payload bytes that parse as a PageHeader prefix followed by a thrift list
+    # header claiming ~2^31 elements: the candidate parse must stay bounded
+    n = 200_000
+    pat = np.frombuffer(bytes([0x15, 0x00, 0x15, 0x00, 0x19, 0xF5, 0xFF, 0xFF]), dtype=np.int64)[0]
+    v = np.full(n, pat, dtype=np.int64)
+    v[1::2] = 0x0101010101010101
+    data = W.write_file([W.Column("x", W.INT64, v, rows_per_page=50_000)], n)
+    P.compare_file(data, dec)
