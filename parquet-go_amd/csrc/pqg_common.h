@@ -68,8 +68,37 @@ struct PageDev {
   int32_t not_null;
   int32_t flags;
   int32_t dict_width;      // RLE_DICTIONARY: index bit width byte
+  int32_t hs_rep, hs_def, hs_val;  // hybrid streams of the page (HStream index, -1: none)
   int32_t pad;
 };
+
+// One RLE/bit-packed hybrid stream (hybrid_decoder.go): a page's rep or def
+// levels, its dictionary indices or its RLE booleans.  k_page_setup registers
+// it, k_hybrid_walk turns it into a run table, the expanders read the table.
+struct HStream {
+  const uint8_t* p;  // first byte of the stream
+  int64_t n;         // stream bytes (reads at or past n are EOF)
+  int64_t run_base;  // first RunEnt of the stream's run table
+  int64_t blk_base;  // first entry of its block index (run of value k*kHBlock)
+  int32_t page;      // PageDev index
+  int32_t kind;      // 0 rep, 1 def, 2 dictionary indices, 3 RLE booleans
+  int32_t w;         // bit width (1..32)
+  int32_t count;     // values wanted (levels: NumValues; values: an upper bound of notNull)
+  // walker results
+  int32_t n_runs;
+  int32_t produced;  // values available before the end of the stream / an error
+  int32_t status;    // error met after `produced` values (kOK: none before `count`)
+  int32_t pad;
+};
+
+// Run table entry: start = first value index of the run (bit 31: bit-packed);
+// src = RLE value, or the byte offset of a bit-packed run's payload.
+struct RunEnt {
+  uint32_t start;
+  uint32_t src;
+};
+constexpr uint32_t kRunBP = 0x80000000u;
+constexpr int kHBlock = 512;  // values per block of the block index / expander step
 
 struct JobDev {
   // ---- inputs
@@ -104,6 +133,10 @@ struct JobDev {
   int32_t n_ok;            // candidates whose read phase succeeds
   int32_t brk;             // first ok-rank whose successor is not the next ok candidate
   int32_t first_dict;      // first ok-rank of a dictionary page
+  // ---- K3 hybrid run tables (pqg_levels.hip)
+  int64_t run_cap, run_base;   // RunEnt arena region
+  int64_t blk_cap, blk_base;   // block-index arena region
+  int64_t run_used, blk_used;  // bump allocators (zeroed by the scan)
 };
 
 // Scan tiles of the speculative page-header search.
@@ -120,8 +153,6 @@ struct Cand {
   int32_t type, encoding, num_values, csize, usize;
   int32_t def_len, rep_len, def_enc, rep_enc;
   int32_t status;          // read-phase status, kCOMPLEX: re-parse serially
-  int32_t okrank;          // rank among the tile's candidates with status kOK
-  int32_t pad;
 };
 
 }  // namespace pqg

@@ -10,6 +10,50 @@ constexpr int kWave = 64;
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
+__device__ __forceinline__ int bits_len(uint32_t v) { return v ? 32 - __builtin_clz(v) : 0; }
+
+// getValuesDecoder chunk_reader.go:143-196 (DELTA_*_BYTE_ARRAY are outside this build)
+__device__ __forceinline__ int values_supported(int type, int type_length, int enc) {
+  switch (type) {
+    case 0: return enc == 0 || enc == 3 || enc == 8;
+    case 6: return enc == 0 || enc == 8;
+    case 7: return type_length >= 0 && (enc == 0 || enc == 8);
+    case 3: case 4: case 5: return enc == 0 || enc == 8;
+    case 1: case 2: return enc == 0 || enc == 5 || enc == 8;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ uint32_t rd_u32(const uint8_t* p) {
+  return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+
+// One lane's byte reader over [p, p+n): 16-byte granules cached in registers
+// (a granule holding a byte < n lies in mapped memory).  -1 past the end.
+struct LaneBytes {
+  const uint8_t* p;
+  int64_t n;
+  uintptr_t gaddr;
+  uint4 g;
+  __device__ __forceinline__ void init(const uint8_t* p_, int64_t n_) {
+    p = p_;
+    n = n_;
+    gaddr = 0;
+  }
+  __device__ __forceinline__ int get(int64_t i) {
+    if (i < 0 || i >= n) return -1;
+    const uintptr_t a = (uintptr_t)(p + i);
+    const uintptr_t ga = a & ~(uintptr_t)15;
+    if (ga != gaddr) {
+      g = *(const uint4*)ga;
+      gaddr = ga;
+    }
+    const int w = (int)((a >> 2) & 3);
+    const uint32_t d = w == 0 ? g.x : w == 1 ? g.y : w == 2 ? g.z : g.w;
+    return (int)((d >> (8 * (a & 3))) & 0xff);
+  }
+};
+
 // Bounds-checked byte read of a device buffer.
 __device__ __forceinline__ int get_byte(const uint8_t* p, int64_t n, int64_t i) {
   return (i >= 0 && i < n) ? (int)p[i] : -1;

@@ -18,7 +18,9 @@
 #include "pqg_common.h"
 
 namespace pqg {
-__global__ void k_page_cands(JobDev* jobs, int n_jobs, int* tile_count, int* tile_okc, Cand* cands);
+__global__ void k_page_cands(JobDev* jobs, int n_jobs, int* tile_count, int* tile_okc, int64_t* cand_pos);
+__global__ void k_cand_parse(JobDev* jobs, int n_jobs, int64_t total_tiles, const int* tile_count, int* tile_okc,
+                             const int64_t* cand_pos, Cand* cands);
 __global__ void k_tile_scan(JobDev* jobs, const int* tile_count, const int* tile_okc, int* tile_off, int* tile_okoff);
 __global__ void k_cand_link(JobDev* jobs, int n_jobs, int64_t total_tiles, const int* tile_count,
                             const int* tile_off, const int* tile_okoff, const Cand* cands, int* succ, int* idx2slot,
@@ -29,11 +31,16 @@ __global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs);
 __global__ void k_page_list(JobDev* jobs, int n_jobs, int* list, int list_cap, int* total, int* queues);
 __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                          uint8_t* scratch);
-__global__ void k_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
-                         uint8_t* scratch, uint8_t* def_arena, uint8_t* rep_arena);
+__global__ void k_page_setup(JobDev* jobs, PageDev* pages, const int* list, const int* total, uint8_t* scratch,
+                             HStream* streams);
+__global__ void k_hybrid_walk(const PageDev* pages, const int* list, const int* total, HStream* streams,
+                              RunEnt* runs, int32_t* blks);
+__global__ void k_levels_expand(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                                const HStream* streams, const RunEnt* runs, const int32_t* blks, uint8_t* def_arena,
+                                uint8_t* rep_arena);
 __global__ void k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch);
 __global__ void k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
-                         uint8_t* value_arena);
+                         uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const int32_t* blks);
 __global__ void k_finalize(JobDev* jobs, int n_jobs, PageDev* pages);
 }  // namespace pqg
 
@@ -65,8 +72,8 @@ struct DevBuf {
   }
 };
 
-constexpr int kStages = 7;
-// stages timed by pqg_last_timings: scan (K1a-e), list, snappy, levels, nn_scan, values, finalize
+constexpr int kStages = 9;
+// stages timed by pqg_last_timings: scan (K1a-e), list, snappy, setup, walk, levels, nn_scan, values, finalize
 
 int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
@@ -88,13 +95,14 @@ struct pqg_ctx {
   hipStream_t stream = nullptr;
   int num_cus = 256;
   DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
-  DevBuf tile_count, tile_okc, tile_off, tile_okoff, cands, succ, idx2slot, ok2slot, order;  // K1 page scan
+  DevBuf tile_count, tile_okc, tile_off, tile_okoff, cand_pos, cands, succ, idx2slot, ok2slot, order;  // K1
+  DevBuf streams, runs, blks;  // K3 hybrid run tables
   int64_t total_tiles = 0;
   JobDev* h_jobs = nullptr;  // pinned
   int h_jobs_cap = 0;
   std::vector<pqg_chunk_job> cur;       // jobs of the in-flight batch
   std::vector<JobDev> plan;             // per-job capacities used
-  std::vector<int64_t> force_pages, force_slots, force_scratch, force_values;
+  std::vector<int64_t> force_pages, force_slots, force_scratch, force_values, force_runs, force_blks;
   int n_jobs = 0;
   int64_t list_cap = 0;
   hipEvent_t ev[kStages + 1];
@@ -155,7 +163,7 @@ void pqg_ctx_destroy(pqg_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (auto& e : c->ev) hipEventDestroy(e);
   for (DevBuf* b : {&c->jobs, &c->pages, &c->list, &c->counters, &c->def_arena, &c->rep_arena, &c->value_arena,
-                    &c->scratch, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cands, &c->succ, &c->idx2slot,
+                    &c->scratch, &c->streams, &c->runs, &c->blks, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
                     &c->ok2slot, &c->order})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
@@ -196,7 +204,8 @@ static int plan_batch(pqg_ctx* c) {
     c->h_jobs_cap = std::max(n, 64);
     if (hipHostMalloc((void**)&c->h_jobs, sizeof(JobDev) * (size_t)c->h_jobs_cap) != hipSuccess) return PQG_ERR_HIP;
   }
-  int64_t page_total = 0, slot_total = 0, value_total = 0, scratch_total = 0, tile_total = 0;
+  int64_t page_total = 0, slot_total = 0, value_total = 0, scratch_total = 0, tile_total = 0, run_total = 0,
+          blk_total = 0;
   c->plan.resize((size_t)n);
   for (int i = 0; i < n; i++) {
     const pqg_chunk_job& in = c->cur[(size_t)i];
@@ -239,6 +248,18 @@ static int plan_batch(pqg_ctx* c) {
     d.dict_page = -1;
     d.error_page = -1;
     const int64_t lim = std::max<int64_t>(0, std::min(in.total_compressed_size, in.data_len));
+    // hybrid run tables: a stream of n bytes has at most n/2 + 2 runs, and a
+    // page at most three streams (see reg_stream)
+    int64_t rcap = (in.total_compressed_size + xcap) / 2 + 6 * pcap + 64;
+    if (c->force_runs[(size_t)i] > 0) rcap = c->force_runs[(size_t)i];
+    d.run_cap = rcap;
+    d.run_base = run_total;
+    run_total += rcap;
+    int64_t bcap = 3 * (scap / kHBlock + 2 * pcap) + 64;
+    if (c->force_blks[(size_t)i] > 0) bcap = c->force_blks[(size_t)i];
+    d.blk_cap = bcap;
+    d.blk_base = blk_total;
+    blk_total += bcap;
     d.tile_base = tile_total;
     d.n_tiles = (int32_t)((lim + kScanTile - 1) / kScanTile);
     tile_total += d.n_tiles;
@@ -253,10 +274,13 @@ static int plan_batch(pqg_ctx* c) {
       c->tile_off.grow(sizeof(int) * (size_t)tile_total + 64) || c->tile_okc.grow(sizeof(int) * (size_t)tile_total + 64) ||
       c->tile_okoff.grow(sizeof(int) * (size_t)tile_total + 64) ||
       c->ok2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
+      c->cand_pos.grow(sizeof(int64_t) * (size_t)tile_total * kCandPerTile + 64) ||
       c->cands.grow(sizeof(Cand) * (size_t)tile_total * kCandPerTile + 64) ||
       c->succ.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->idx2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
-      c->order.grow(sizeof(int) * (size_t)page_total + 64))
+      c->order.grow(sizeof(int) * (size_t)page_total + 64) ||
+      c->streams.grow(sizeof(HStream) * 3 * (size_t)page_total + 64) || c->runs.grow(sizeof(RunEnt) * (size_t)run_total + 64) ||
+      c->blks.grow(sizeof(int32_t) * (size_t)blk_total + 64))
     return PQG_ERR_HIP;
   c->total_tiles = tile_total;
   return hip_ok(hipMemcpyAsync(c->jobs.p, c->h_jobs, sizeof(JobDev) * (size_t)n, hipMemcpyHostToDevice, c->stream));
@@ -269,7 +293,10 @@ static int launch_pipeline(pqg_ctx* c) {
   int* list = (int*)c->list.p;
   int* ctr = (int*)c->counters.p;  // [0] total pages, [8..15] queues
   uint8_t* scratch = (uint8_t*)c->scratch.p;
-  const int waves = c->num_cus * 8;
+  // page-queue kernels: one wave per page; enough waves per SIMD to hide the
+  // dependent HBM reads of the run walks (bounded by VGPRs / LDS per kernel)
+  const int waves = c->num_cus * 20;
+  const int snappy_waves = c->num_cus * 4;  // 33 KiB LDS each
   hipStream_t s = c->stream;
   if (c->timed) hipEventRecord(c->ev[0], s);
   const int64_t nt = c->total_tiles;
@@ -278,7 +305,12 @@ static int launch_pipeline(pqg_ctx* c) {
   Cand* cands = (Cand*)c->cands.p;
   int* tokc = (int*)c->tile_okc.p;
   int* tokoff = (int*)c->tile_okoff.p;
-  if (nt > 0) hipLaunchKernelGGL(k_page_cands, dim3((unsigned)nt), dim3(256), 0, s, jobs, n, tcount, tokc, cands);
+  if (nt > 0) {
+    int64_t* cpos = (int64_t*)c->cand_pos.p;
+    hipLaunchKernelGGL(k_page_cands, dim3((unsigned)nt), dim3(256), 0, s, jobs, n, tcount, tokc, cpos);
+    hipLaunchKernelGGL(k_cand_parse, dim3((unsigned)((nt * kCandPerTile + 255) / 256)), dim3(256), 0, s, jobs, n, nt,
+                       tcount, tokc, cpos, cands);
+  }
   hipLaunchKernelGGL(k_tile_scan, dim3(n), dim3(1024), 0, s, jobs, tcount, tokc, toff, tokoff);
   if (nt > 0)
     hipLaunchKernelGGL(k_cand_link, dim3((unsigned)((nt * kCandPerTile + 255) / 256)), dim3(256), 0, s, jobs, n, nt,
@@ -293,18 +325,28 @@ static int launch_pipeline(pqg_ctx* c) {
   bool any_comp = false;
   for (int i = 0; i < n; i++) any_comp |= c->cur[(size_t)i].col.codec != PQG_CODEC_UNCOMPRESSED;
   if (any_comp)
-    hipLaunchKernelGGL(k_snappy, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 8, scratch);
+    hipLaunchKernelGGL(k_snappy, dim3(snappy_waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 8, scratch);
   if (c->timed) hipEventRecord(c->ev[3], s);
-  hipLaunchKernelGGL(k_levels, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 9, scratch,
-                     (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p);
+  HStream* streams = (HStream*)c->streams.p;
+  RunEnt* runs = (RunEnt*)c->runs.p;
+  int32_t* blks = (int32_t*)c->blks.p;
+  const unsigned lane_blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((c->list_cap + 255) / 256, c->num_cus * 4));
+  hipLaunchKernelGGL(k_page_setup, dim3(lane_blocks), dim3(256), 0, s, jobs, pages, list, ctr, scratch, streams);
   if (c->timed) hipEventRecord(c->ev[4], s);
-  hipLaunchKernelGGL(k_nn_scan, dim3(n), dim3(256), 0, s, jobs, pages, scratch);
+  const unsigned walk_blocks =
+      (unsigned)std::max<int64_t>(1, std::min<int64_t>((3 * c->list_cap + 255) / 256, c->num_cus * 8));
+  hipLaunchKernelGGL(k_hybrid_walk, dim3(walk_blocks), dim3(256), 0, s, pages, list, ctr, streams, runs, blks);
   if (c->timed) hipEventRecord(c->ev[5], s);
-  hipLaunchKernelGGL(k_values, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 10,
-                     (uint8_t*)c->value_arena.p);
+  hipLaunchKernelGGL(k_levels_expand, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 9, streams, runs, blks,
+                     (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p);
   if (c->timed) hipEventRecord(c->ev[6], s);
-  hipLaunchKernelGGL(k_finalize, dim3(n), dim3(256), 0, s, jobs, n, pages);
+  hipLaunchKernelGGL(k_nn_scan, dim3(n), dim3(256), 0, s, jobs, pages, scratch);
   if (c->timed) hipEventRecord(c->ev[7], s);
+  hipLaunchKernelGGL(k_values, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 10,
+                     (uint8_t*)c->value_arena.p, streams, runs, blks);
+  if (c->timed) hipEventRecord(c->ev[8], s);
+  hipLaunchKernelGGL(k_finalize, dim3(n), dim3(256), 0, s, jobs, n, pages);
+  if (c->timed) hipEventRecord(c->ev[9], s);
   return hip_ok(hipGetLastError());
 }
 
@@ -323,6 +365,8 @@ int pqg_decode_chunks_async(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs) {
   c->force_slots.assign((size_t)n_jobs, 0);
   c->force_scratch.assign((size_t)n_jobs, 0);
   c->force_values.assign((size_t)n_jobs, 0);
+  c->force_runs.assign((size_t)n_jobs, 0);
+  c->force_blks.assign((size_t)n_jobs, 0);
   if (n_jobs == 0) return PQG_OK;
   int e = plan_batch(c);
   if (e) return e;
@@ -350,6 +394,8 @@ int pqg_sync(pqg_ctx* c, pqg_chunk_result* results, int n_jobs) {
       c->force_scratch[(size_t)i] = std::max<int64_t>(d.need_scratch + 1024, d.scratch_cap);
       int64_t nv = std::max<int64_t>(d.num_values, d.num_slots);
       c->force_values[(size_t)i] = std::max<int64_t>(nv * std::max(d.value_width, 1) + 64, d.value_cap);
+      c->force_runs[(size_t)i] = std::max<int64_t>(d.run_used + 64, d.run_cap);
+      c->force_blks[(size_t)i] = std::max<int64_t>(d.blk_used + 64, d.blk_cap);
     }
     if (!retry) break;
     int e = plan_batch(c);
@@ -452,13 +498,18 @@ int pqg_bench_decode(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs, int iter
   int e = pqg_decode_chunks(c, jobs, n_jobs, res.data());
   if (e) return e;
   // freeze the capacities found by the first call
-  std::vector<int64_t> fp(c->force_pages), fs(c->force_slots), fx(c->force_scratch), fv(c->force_values);
+  std::vector<int64_t> fp(c->force_pages), fs(c->force_slots), fx(c->force_scratch), fv(c->force_values),
+      fr(c->force_runs), fb(c->force_blks);
   for (int i = 0; i < n_jobs; i++) {
     fp[(size_t)i] = c->h_jobs[i].page_cap;
     fs[(size_t)i] = c->h_jobs[i].slot_cap;
     fx[(size_t)i] = c->h_jobs[i].scratch_cap;
     fv[(size_t)i] = c->h_jobs[i].value_cap;
+    fr[(size_t)i] = c->h_jobs[i].run_cap;
+    fb[(size_t)i] = c->h_jobs[i].blk_cap;
   }
+  c->force_runs = fr;
+  c->force_blks = fb;
   c->force_pages = fp;
   c->force_slots = fs;
   c->force_scratch = fx;

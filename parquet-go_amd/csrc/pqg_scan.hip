@@ -1,0 +1,707 @@
+// pqg_scan.hip — K1: page-header scan of every chunk (readPages,
+// chunk_reader.go:206-284) and the compact page list.
+#include <hip/hip_runtime.h>
+
+#include "pqg_common.h"
+#include "pqg_device.h"
+#include "pqg_thrift.h"
+
+namespace pqg {
+
+// Byte source over the LDS window, for the thrift reader of the serial walk.
+struct WinSrc {
+  Window w;  // by value: the parser state stays in registers
+  __device__ int get(int64_t i) { return w.get(i); }
+};
+
+
+// ============================================================================
+// K1: page-header scan.
+//
+// readPages (chunk_reader.go:206-284) walks the chunk serially: parse a
+// PageHeader at pos, then pos = payload + CompressedPageSize (or
+// DataPageOffset after the dictionary page, :243-249).  A serial walk costs
+// one dependent HBM round trip per page, so the GPU finds the pages
+// speculatively instead:
+//   K1a k_page_cands  every byte position p of every chunk is tested for the
+//                     compact-protocol prefix of a PageHeader (field 1 `type`
+//                     i32 with a 1-byte value, then field 2 i32: 15 xx 15);
+//                     each hit is parsed by one lane and classified.
+//   K1b k_tile_scan   per-chunk exclusive scan of the per-tile hit counts.
+//   K1c k_cand_link   each candidate finds the candidate at its next-page
+//                     position (its successor).
+//   K1d k_page_chain  pages = the successor chain from position 0.  False
+//                     candidates (payload bytes that happen to parse) are
+//                     never on it.  Pages are written in chain order with the
+//                     slot / scratch prefix sums.
+//   K1e k_scan_pages  the serial walk, run only for chunks the speculative
+//                     path cannot settle (a chain position with no candidate,
+//                     a tile with more than kCandPerTile hits, deep thrift
+//                     nesting): results are identical by construction, since
+//                     both paths share classify_page.
+// ============================================================================
+
+// Read-phase classification of one parsed header (readPages :216-272 with
+// dictPageReader.read page_dict.go:30-64, dataPageReaderV1.read
+// page_v1.go:79-108, dataPageReaderV2.read page_v2.go:73-129).  `dict_seen`:
+// an earlier page of the walk was a dictionary page.  Sets *next to the
+// position of the following page and *comp to the scratch bytes (16-rounded)
+// the page's decompressed block needs.
+__device__ int classify_page(const JobDev& job, const PageHdr& h, int e, int64_t payload, bool dict_seen,
+                             PageDev& pg, int64_t* next, int64_t* comp) {
+  *comp = 0;
+  *next = payload;
+  pg.page_type = h.type;
+  pg.encoding = h.encoding;
+  pg.num_values = 0;
+  pg.csize = h.csize;
+  pg.usize = h.usize;
+  pg.def_len = h.v2_def_len;
+  pg.rep_len = h.v2_rep_len;
+  pg.def_enc = h.def_enc;
+  pg.rep_enc = h.rep_enc;
+  if (e != kOK) return e;
+  if (h.type == 2) {  // DICTIONARY_PAGE (page_dict.go:30-64, chunk_reader.go:221-251)
+    pg.num_values = h.has_dict ? h.num_values : 0;
+    if (dict_seen) e = kDICT_PAGE;
+    else if (job.type == 0 || (job.type == 7 && job.type_length < 0)) e = kUNSUPPORTED;
+    else if (!h.has_dict || h.num_values < 0) e = kPAGE_HEADER;
+    else if (h.encoding != 0 && h.encoding != 2) e = kUNSUPPORTED;
+    else if (h.csize < 0 || h.usize < 0) e = kPAGE_HEADER;
+    else if (job.data_len - payload < (int64_t)h.csize) e = kSIZE;
+    else if (job.codec == 0) { if (h.csize != h.usize) e = kSIZE; }
+    else if (job.codec == 1) *comp = ((int64_t)h.usize + 15) & ~(int64_t)15;
+    else e = kUNSUPPORTED;
+    *next = payload + h.csize;
+    if (e == kOK && job.has_dict_off) *next = job.data_page_offset;
+    if (e != kOK) *comp = 0;
+  } else if (h.type == 0) {  // DATA_PAGE (page_v1.go:57-108)
+    pg.num_values = h.has_dph ? h.num_values : 0;
+    int enc = h.encoding == 2 ? 8 : h.encoding;
+    pg.encoding = enc;
+    if (!h.has_dph) e = kPAGE_HEADER;
+    else if (job.max_rep > 0 && h.rep_enc != 3) e = kUNSUPPORTED;
+    else if (job.max_def > 0 && h.def_enc != 3) e = kUNSUPPORTED;
+    else if (h.num_values < 0) e = kPAGE_HEADER;
+    else if (h.csize < 0 || h.usize < 0) e = kPAGE_HEADER;
+    else if (job.data_len - payload < (int64_t)h.csize) e = kSIZE;
+    else if (job.codec == 0 && h.csize != h.usize) e = kSIZE;
+    else if (job.codec != 0 && job.codec != 1) e = kUNSUPPORTED;
+    else if (job.codec == 0 && !values_supported(job.type, job.type_length, enc)) e = kUNSUPPORTED;
+    if (e == kOK && job.codec == 1) *comp = ((int64_t)h.usize + 15) & ~(int64_t)15;
+    *next = payload + h.csize;
+  } else if (h.type == 3) {  // DATA_PAGE_V2 (page_v2.go:56-129)
+    pg.num_values = h.has_v2 ? h.num_values : 0;
+    int enc = h.encoding == 2 ? 8 : h.encoding;
+    pg.encoding = enc;
+    int32_t levels = (int32_t)((uint32_t)h.v2_rep_len + (uint32_t)h.v2_def_len);
+    int32_t cs = (int32_t)((uint32_t)h.csize - (uint32_t)levels);
+    int32_t us = (int32_t)((uint32_t)h.usize - (uint32_t)levels);
+    int64_t body = payload + (levels > 0 ? levels : 0);
+    if (!h.has_v2) e = kPAGE_HEADER;
+    else if (h.num_values < 0 || h.v2_rep_len < 0 || h.v2_def_len < 0) e = kPAGE_HEADER;
+    else if (!values_supported(job.type, job.type_length, enc)) e = kUNSUPPORTED;
+    else if (levels > 0 && job.data_len - payload < (int64_t)levels) e = kEOF;
+    else if (cs < 0 || us < 0) e = kPAGE_HEADER;
+    else if (job.data_len - body < (int64_t)cs) e = kSIZE;
+    else if (job.codec == 0 && cs != us) e = kSIZE;
+    else if (job.codec != 0 && job.codec != 1) e = kUNSUPPORTED;
+    if (e == kOK && job.codec == 1) *comp = ((int64_t)us + 15) & ~(int64_t)15;
+    *next = body + cs;
+  } else {
+    e = kUNSUPPORTED;  // "DATA_PAGE or DATA_PAGE_V2 type supported"
+  }
+  return e;
+}
+
+__device__ __forceinline__ void init_page(PageDev& pg, int j, int64_t pos, int64_t payload) {
+  pg.header_offset = pos;
+  pg.payload_offset = payload;
+  pg.slot_offset = 0;
+  pg.value_offset = 0;
+  pg.scratch_offset = -1;
+  pg.block = nullptr;
+  pg.block_len = 0;
+  pg.rep = pg.def = pg.val = nullptr;
+  pg.rep_n = pg.def_n = pg.val_n = 0;
+  pg.job = j;
+  pg.read_status = kOK;
+  pg.decode_status = kOK;
+  pg.not_null = 0;
+  pg.flags = 0;
+  pg.dict_width = 0;
+  pg.pad = 0;
+}
+
+__device__ __forceinline__ void init_job_results(JobDev& job) {
+  job.num_pages = 0;
+  job.dict_page = -1;
+  job.scan_status = kOK;
+  job.need_scratch = 0;
+  job.num_slots = 0;
+  job.dict_data = nullptr;
+  job.dict_count = 0;
+  job.dict_len = 0;
+  job.dict_offs = nullptr;
+  job.status = kOK;
+  job.error_page = -1;
+  job.flags = 0;
+  job.run_used = 0;
+  job.blk_used = 0;
+}
+
+// ---- K1a ------------------------------------------------------------------
+// Byte source of the per-lane candidate parse.  Reads stop at `limit`
+// (kCandParseBytes past the candidate): a header that needs more is left to
+// the serial walk (`hit`), so a garbage candidate cannot run away through the
+// chunk (e.g. a thrift list header claiming 2^31 elements).
+constexpr int64_t kCandParseBytes = 1024;
+struct GlobalSrc {
+  const uint8_t* p;
+  int64_t n, limit;
+  bool hit;
+  uintptr_t gaddr;  // 16-byte granule held in `g` (0: none)
+  uint4 g;
+  __device__ int get(int64_t i) {
+    if (i >= limit && i < n) {
+      hit = true;
+      return -1;
+    }
+    if (i < 0 || i >= n) return -1;
+    const uintptr_t a = (uintptr_t)(p + i);
+    const uintptr_t ga = a & ~(uintptr_t)15;
+    if (ga != gaddr) {  // the granule holds byte i < n: mapped
+      g = *(const uint4*)ga;
+      gaddr = ga;
+    }
+    const int w = (int)((a >> 2) & 3);
+    const uint32_t d = w == 0 ? g.x : w == 1 ? g.y : w == 2 ? g.z : g.w;
+    return (int)((d >> (8 * (a & 3))) & 0xff);
+  }
+};
+
+__device__ __forceinline__ bool has_byte_15(uint32_t x) {
+  uint32_t y = x ^ 0x15151515u;
+  return ((y - 0x01010101u) & ~y & 0x80808080u) != 0;
+}
+
+constexpr int kCandFrames = 4, kCandLast = 8;
+
+// One lane parses and classifies the candidate at position p (kept out of
+// line: the scan loop around it must stay small).
+__device__ __noinline__ void parse_candidate(const JobDev& job, int64_t p, SkipFrame* frames, int16_t* lasts,
+                                             Cand* out) {
+  Compact<GlobalSrc> c;
+  c.src = GlobalSrc{job.data, job.data_len, p + kCandParseBytes, false, 0, make_uint4(0, 0, 0, 0)};
+  // Structural pre-check: every thrift writer of PageHeader emits fields 1, 2,
+  // 3 in id order with short-form i32 headers (15 t 15 <varint> 15).  A
+  // candidate without that shape is not parsed: it is marked kCOMPLEX, which
+  // sends the chunk to the serial walk only if a page link ever lands on it.
+  {
+    int64_t q = p + 3;
+    int b = 0x80;
+    for (int k = 0; k < 5 && (b & 0x80); k++) b = c.src.get(q++);
+    if (b < 0 || (b & 0x80) || c.src.get(q) != 0x15) {
+      Cand cd;
+      cd.pos = p;
+      cd.next = p;
+      cd.payload = p;
+      cd.comp = 0;
+      cd.type = cd.encoding = cd.num_values = cd.csize = cd.usize = 0;
+      cd.def_len = cd.rep_len = cd.def_enc = cd.rep_enc = 0;
+      cd.status = kCOMPLEX;
+      *out = cd;
+      return;
+    }
+  }
+  c.pos = p;
+  c.frames = frames;
+  c.last = lasts;
+  c.nlast = 0;
+  c.last_id = 0;
+  c.bool_set = c.bool_val = false;
+  c.fcap = kCandFrames;
+  c.lcap = kCandLast;
+  PageHdr h;
+  int e = c.read_page_header(&h);
+  PageDev pg;
+  int64_t next, comp;
+  e = classify_page(job, h, e, c.pos, false, pg, &next, &comp);
+  if (c.overflow || c.src.hit) e = kCOMPLEX;
+  Cand cd;
+  cd.pos = p;
+  cd.next = next;
+  cd.payload = c.pos;
+  cd.comp = comp;
+  cd.type = pg.page_type;
+  cd.encoding = pg.encoding;
+  cd.num_values = pg.num_values;
+  cd.csize = pg.csize;
+  cd.usize = pg.usize;
+  cd.def_len = pg.def_len;
+  cd.rep_len = pg.rep_len;
+  cd.def_enc = pg.def_enc;
+  cd.rep_enc = pg.rep_enc;
+  cd.status = e;
+  *out = cd;
+}
+
+__global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, int n_jobs, int* tile_count, int* tile_okc,
+                                                    int64_t* cand_pos) {
+  __shared__ int cnt;
+  __shared__ int job_s;
+  __shared__ int64_t loc[kCandPerTile];
+  const int tid = threadIdx.x;
+  const int64_t tile = blockIdx.x;
+  if (tid == 0) {
+    cnt = 0;
+    int lo = 0, hi = n_jobs - 1;  // last job with tile_base <= tile
+    while (lo < hi) {
+      int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].tile_base <= tile) lo = mid; else hi = mid - 1;
+    }
+    job_s = lo;
+  }
+  __syncthreads();
+  const JobDev& job = jobs[job_s];
+  const int64_t lim = job.tcs < job.data_len ? job.tcs : job.data_len;
+  const int64_t t0 = (tile - job.tile_base) * kScanTile;
+  const int64_t t1 = t0 + kScanTile < lim ? t0 + kScanTile : lim;
+  const uint8_t* base = job.data;
+  const int64_t data_len = job.data_len;
+  const uintptr_t a0 = (uintptr_t)(base + t0) & ~(uintptr_t)15;
+  for (int64_t off = (int64_t)tid * 16;; off += 256 * 16) {
+    const uintptr_t a = a0 + off;
+    const int64_t p0 = (int64_t)(a - (uintptr_t)base);
+    if (p0 >= t1) break;
+    // the 16-byte granule holds a position < t1 <= data_len, so it is mapped
+    const uint4 v = *(const uint4*)a;
+    if (!(has_byte_15(v.x) || has_byte_15(v.y) || has_byte_15(v.z) || has_byte_15(v.w))) continue;
+    // bytes 16, 17 (lookahead of the last two positions), read only when
+    // byte 14 or 15 is 0x15; 0xff (no match) past the end of the buffer
+    uint32_t nx = 0xffffu;
+    if (((v.w >> 16) & 0xff) == 0x15 || (v.w >> 24) == 0x15) {
+      const int64_t q = p0 + 16;
+      nx = (q < data_len ? (uint32_t)base[q] : 0xffu) | (q + 1 < data_len ? (uint32_t)base[q + 1] : 0xffu) << 8;
+    }
+    const uint32_t w5[5] = {v.x, v.y, v.z, v.w, nx};
+    uint32_t mask = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t c0 = (w5[k >> 2] >> (8 * (k & 3))) & 0xff;
+      const uint32_t c1 = (w5[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xff;
+      const uint32_t c2 = (w5[(k + 2) >> 2] >> (8 * ((k + 2) & 3))) & 0xff;
+      mask |= (uint32_t)(c0 == 0x15 && (c1 & 0xf9) == 0 && c2 == 0x15) << k;
+    }
+    // positions outside [t0, t1) belong to the neighbouring tiles
+    while (mask) {
+      const int k = __builtin_ctz(mask);
+      mask &= mask - 1;
+      const int64_t p = p0 + k;
+      if (p < t0 || p >= t1) continue;
+      const int slot = atomicAdd(&cnt, 1);
+      if (slot < kCandPerTile) loc[slot] = p;  // beyond: overflow, the chunk takes the serial walk
+    }
+  }
+  __syncthreads();
+  const int n = cnt;
+  if (tid == 0) {
+    tile_count[tile] = n > kCandPerTile ? kCandPerTile + 1 : n;
+    tile_okc[tile] = 0;  // counted by k_cand_parse
+  }
+  if (n <= kCandPerTile && tid < n) {  // rank sort by position (positions are distinct)
+    const int64_t me = loc[tid];
+    int rank = 0;
+    for (int k = 0; k < n; k++) rank += loc[k] < me;
+    cand_pos[tile * kCandPerTile + rank] = me;
+  }
+}
+
+// ---- K1a' ------------------------------------------------------------------
+// One lane per candidate slot: parse + classify (kept apart from the byte scan
+// so that the scan has no scratch and runs at full occupancy).
+__global__ void __launch_bounds__(256) k_cand_parse(JobDev* jobs, int n_jobs, int64_t total_tiles,
+                                                    const int* tile_count, int* tile_okc, const int64_t* cand_pos,
+                                                    Cand* cands) {
+  __shared__ SkipFrame frames[256][kCandFrames];
+  __shared__ int16_t lasts[256][kCandLast];
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tile = g / kCandPerTile;
+  const int s = (int)(g % kCandPerTile);
+  if (tile >= total_tiles) return;
+  const int cntv = tile_count[tile];
+  if (s >= cntv || cntv > kCandPerTile) return;
+  int lo = 0, hi = n_jobs - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].tile_base <= tile) lo = mid; else hi = mid - 1;
+  }
+  Cand* out = &cands[tile * kCandPerTile + s];
+  parse_candidate(jobs[lo], cand_pos[tile * kCandPerTile + s], frames[threadIdx.x], lasts[threadIdx.x], out);
+  if (out->status == kOK) atomicAdd(&tile_okc[tile], 1);
+}
+
+// ---- K1b ------------------------------------------------------------------
+// Per-chunk exclusive scans of the tile candidate counts (all, and ok-status).
+__global__ void __launch_bounds__(1024) k_tile_scan(JobDev* jobs, const int* tile_count, const int* tile_okc,
+                                                    int* tile_off, int* tile_okoff) {
+  __shared__ int64_t part[17];
+  __shared__ int ovf;
+  JobDev& job = jobs[blockIdx.x];
+  const int tid = threadIdx.x;
+  if (tid == 0) ovf = 0;
+  __syncthreads();
+  const int nt = job.n_tiles;
+  const int64_t tb = job.tile_base;
+  // each thread sums a contiguous segment, one block scan, then writes
+  const int seg = (nt + 1023) / 1024;
+  const int s0 = tid * seg, s1 = min(nt, s0 + seg);
+  int64_t sum = 0, oks = 0;
+  bool bad = false;
+  for (int t = s0; t < s1; t++) {
+    int c = tile_count[tb + t];
+    bad |= c > kCandPerTile;
+    sum += c;
+    oks += tile_okc[tb + t];
+  }
+  if (bad) ovf = 1;
+  int64_t total, ok_total;
+  int64_t ex = block_excl_scan<1024>(sum, &total, part);
+  int64_t exo = block_excl_scan<1024>(oks, &ok_total, part);
+  for (int t = s0; t < s1; t++) {
+    tile_off[tb + t] = (int)ex;
+    tile_okoff[tb + t] = (int)exo;
+    ex += tile_count[tb + t];
+    exo += tile_okc[tb + t];
+  }
+  if (tid == 0) {
+    init_job_results(job);
+    job.n_cands = (int32_t)min(total, (int64_t)INT32_MAX);
+    job.n_ok = (int32_t)min(ok_total, (int64_t)INT32_MAX);
+    job.scan_fallback = (ovf || total > INT32_MAX / 2) ? 1 : 0;
+    job.brk = INT32_MAX;
+    job.first_dict = INT32_MAX;
+  }
+}
+
+// successor codes
+constexpr int kSuccEnd = -1;      // next >= TotalCompressedSize: the walk ends
+constexpr int kSuccTerm = -2;     // this page's read phase fails: the walk stops here
+constexpr int kSuccMissing = -3;  // no candidate at the next position
+constexpr int kSuccComplex = -4;  // candidate needs the serial parse
+
+// ---- K1c ------------------------------------------------------------------
+// One lane per candidate slot (kCandPerTile lanes per tile).  Candidates are
+// numbered by position (index i) and, among those whose read phase succeeds,
+// by ok-rank r.  A failing candidate can only END a walk, so in-header false
+// hits (`15 00 15 06 ..` inside a DataPageHeader), which fail to classify,
+// do not break the fast path: it checks that each ok candidate links to the
+// ok candidate of the next rank.
+__global__ void __launch_bounds__(256) k_cand_link(JobDev* jobs, int n_jobs, int64_t total_tiles,
+                                                   const int* tile_count, const int* tile_off,
+                                                   const int* tile_okoff, const Cand* cands, int* succ,
+                                                   int* idx2slot, int* ok2slot) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tile = g / kCandPerTile;
+  const int s = (int)(g % kCandPerTile);
+  if (tile >= total_tiles) return;
+  const int cntv = tile_count[tile];
+  if (s >= cntv || cntv > kCandPerTile) return;
+  int lo = 0, hi = n_jobs - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].tile_base <= tile) lo = mid; else hi = mid - 1;
+  }
+  JobDev& job = jobs[lo];
+  if (job.scan_fallback) return;
+  const Cand& cd = cands[tile * kCandPerTile + s];
+  const int64_t tb = job.tile_base;
+  const int i = tile_off[tile] + s;
+  const int slot = (int)((tile - tb) * kCandPerTile + s);
+  idx2slot[tb * kCandPerTile + i] = slot;
+  const bool ok = cd.status == kOK;
+  int okr = 0;  // ok candidates before this one in the tile
+  for (int k = 0; k < s; k++) okr += cands[tile * kCandPerTile + k].status == kOK;
+  const int r = tile_okoff[tile] + okr;
+  if (ok) ok2slot[tb * kCandPerTile + r] = slot;
+  int code;
+  bool next_rank = false;  // successor is the ok candidate of rank r+1
+  if (cd.status == kCOMPLEX) code = kSuccComplex;
+  else if (!ok) code = kSuccTerm;
+  else if (job.tcs - cd.next <= 0) code = kSuccEnd;
+  else {
+    code = kSuccMissing;
+    const int64_t q = cd.next;
+    const int64_t lim = job.tcs < job.data_len ? job.tcs : job.data_len;
+    if (q >= 0 && q < lim) {
+      const int64_t tq = tb + q / kScanTile;
+      const int c2 = tile_count[tq];
+      const Cand* tc = cands + tq * kCandPerTile;
+      int lo2 = 0, hi2 = (c2 < kCandPerTile ? c2 : kCandPerTile) - 1;  // sorted by pos
+      while (lo2 < hi2) {
+        int mid = (lo2 + hi2) >> 1;
+        if (tc[mid].pos < q) lo2 = mid + 1; else hi2 = mid;
+      }
+      if (hi2 >= 0 && tc[lo2].pos == q) {
+        code = tile_off[tq] + lo2;
+        if (tc[lo2].status == kOK) {
+          int okt = 0;
+          for (int k = 0; k < lo2; k++) okt += tc[k].status == kOK;
+          next_rank = tile_okoff[tq] + okt == r + 1;
+        }
+      }
+    }
+  }
+  succ[tile * kCandPerTile + s] = code;
+  if (i == 0 && cd.pos != 0) atomicOr(&job.scan_fallback, 1);
+  if (ok && !next_rank) atomicMin(&job.brk, r);
+  if (ok && cd.type == 2) atomicMin(&job.first_dict, r);
+}
+
+// ---- K1d ------------------------------------------------------------------
+// The page list = the successor chain from position 0.  Fast path: ok
+// candidates of rank 0..brk, plus the failing page the last one links to.
+// Otherwise a serial walk over the links (false ok candidates between pages)
+// or, when a link has no candidate, the serial header walk (K1e).
+__device__ __forceinline__ bool dict_again(const Cand& c, bool dict_seen) {
+  // readPages :221-223: a second DICTIONARY_PAGE fails with "only one
+  // dictionary" before its own checks (a header that did not parse fails first)
+  return dict_seen && c.type == 2 && c.status != kTHRIFT;
+}
+
+__global__ void __launch_bounds__(1024) k_page_chain(JobDev* jobs, PageDev* pages, const Cand* cands,
+                                                     const int* succ, const int* idx2slot, const int* ok2slot,
+                                                     int* order) {
+  __shared__ int64_t part[17];
+  __shared__ int s_n, s_mode, s_cut, s_status, s_dict, s_extra, s_nok;
+  const int j = blockIdx.x;
+  JobDev& job = jobs[j];
+  const int tid = threadIdx.x;
+  const int64_t lim = job.tcs < job.data_len ? job.tcs : job.data_len;
+  if (job.scan_fallback) return;
+  if (job.tcs <= 0) return;  // the walk reads nothing: no pages
+  if (lim <= 0 || job.n_cands == 0) {
+    if (tid == 0) job.scan_fallback = 1;  // a page must start at 0: let the serial walk classify it
+    return;
+  }
+  const int64_t cb = job.tile_base * kCandPerTile;  // the job's candidate-slot base
+  const int* i2s = idx2slot + cb;
+  const int* o2s = ok2slot + cb;
+  const int b = job.brk;  // < n_ok when index 0 is ok
+  const int d1 = job.first_dict;
+  const Cand& head = cands[cb + i2s[0]];  // at position 0 (checked by k_cand_link)
+  if (tid == 0) {
+    s_cut = INT32_MAX;
+    s_mode = 0;
+    s_dict = -1;
+    s_extra = -1;
+    s_nok = 0;
+  }
+  __syncthreads();
+  if (head.status == kOK && d1 < b) {  // second dictionary page within ranks (d1, b]
+    for (int r = d1 + 1 + tid; r <= b; r += 1024)
+      if (cands[cb + o2s[r]].type == 2) atomicMin(&s_cut, r);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int n = 0, mode = 0;  // mode 0: ok prefix (+ extra), 1: walked (order[]), 2: fallback
+    if (head.status == kCOMPLEX) {
+      mode = 2;
+    } else if (head.status != kOK) {  // the first page fails
+      n = 1;
+      s_extra = i2s[0];
+    } else {
+      if (d1 <= b) s_dict = d1;
+      if (s_cut != INT32_MAX) {
+        n = s_cut + 1;
+        s_nok = n;
+      } else {
+        const int code = succ[cb + o2s[b]];
+        s_nok = b + 1;
+        n = b + 1;
+        if (code == kSuccMissing || code == kSuccComplex) {
+          mode = 2;
+        } else if (code >= 0) {
+          const int ts = i2s[code];
+          const Cand& t = cands[cb + ts];
+          if (t.status == kCOMPLEX) {
+            mode = 2;
+          } else if (t.status != kOK) {  // the walk ends on this failing page
+            s_extra = ts;
+            if (dict_again(t, d1 <= b)) s_cut = n;
+            n++;
+          } else {
+            // false ok candidates between pages: walk the links serially
+            int* ord = order + job.page_base;
+            for (int r = 0; r <= b && r < job.page_cap; r++) ord[r] = o2s[r];
+            bool dict_seen = d1 <= b;
+            int k = b + 1, cur = code;
+            mode = 1;
+            for (;;) {
+              if (k >= job.page_cap) { mode = 2; break; }
+              const int sl = i2s[cur];
+              const Cand& cd = cands[cb + sl];
+              if (cd.status == kCOMPLEX) { mode = 2; break; }
+              ord[k++] = sl;
+              if (dict_again(cd, dict_seen)) { s_cut = k - 1; break; }
+              if (cd.type == 2 && cd.status == kOK) {
+                dict_seen = true;
+                s_dict = k - 1;
+              }
+              const int c2 = succ[cb + sl];
+              if (c2 == kSuccEnd || c2 == kSuccTerm) break;
+              if (c2 < 0) { mode = 2; break; }
+              cur = c2;
+            }
+            n = k;
+          }
+        }
+      }
+    }
+    if (mode == 2) job.scan_fallback = 1;
+    s_n = n;
+    s_mode = mode;
+    s_status = kOK;
+  }
+  __syncthreads();
+  if (s_mode == 2) return;
+  const int n = s_n, mode = s_mode, cut = s_cut, nok = s_nok, extra = s_extra;
+  const int nw = n < job.page_cap ? n : job.page_cap;
+  int64_t slot_carry = 0, scratch_carry = 0;
+  for (int b0 = 0; b0 < n; b0 += 1024) {
+    const int k = b0 + tid;
+    int64_t nv = 0, cp = 0;
+    int st = kOK;
+    const Cand* cd = nullptr;
+    if (k < n) {
+      const int sl = mode == 1 ? order[job.page_base + k] : (k < nok ? o2s[k] : extra);
+      cd = &cands[cb + sl];
+      st = (k == cut) ? kDICT_PAGE : cd->status;
+      cp = (k == cut) ? 0 : cd->comp;
+      if ((cd->type == 0 || cd->type == 3) && st == kOK) nv = cd->num_values;
+      if (st != kOK) s_status = st;  // only the last page can fail
+    }
+    int64_t tot_nv, tot_cp;
+    const int64_t ex_nv = block_excl_scan<1024>(nv, &tot_nv, part);
+    const int64_t ex_cp = block_excl_scan<1024>(cp, &tot_cp, part);
+    if (k < nw) {
+      PageDev pg;
+      init_page(pg, j, cd->pos, cd->payload);
+      pg.page_type = cd->type;
+      pg.encoding = cd->encoding;
+      pg.num_values = cd->num_values;
+      pg.csize = cd->csize;
+      pg.usize = cd->usize;
+      pg.def_len = cd->def_len;
+      pg.rep_len = cd->rep_len;
+      pg.def_enc = cd->def_enc;
+      pg.rep_enc = cd->rep_enc;
+      pg.read_status = st;
+      pg.slot_offset = slot_carry + ex_nv;
+      if (cp > 0) pg.scratch_offset = scratch_carry + ex_cp;
+      pages[job.page_base + k] = pg;
+    }
+    slot_carry += tot_nv;
+    scratch_carry += tot_cp;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    job.num_pages = n;
+    job.dict_page = s_dict;
+    job.scan_status = s_status;
+    job.need_scratch = scratch_carry;
+    job.num_slots = slot_carry;
+    if (n > job.page_cap || slot_carry > job.slot_cap || scratch_carry > job.scratch_cap) job.status = kCAPACITY;
+  }
+}
+
+// ---- K1e: the serial walk (fallback) — one wave per chunk ------------------
+struct ScanShared {
+  uint8_t win[kWin];
+  SkipFrame frames[kMaxFrames];
+  int16_t last[kMaxLast];
+};
+
+__global__ void __launch_bounds__(64) k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs) {
+  __shared__ __attribute__((aligned(16))) ScanShared sh;
+  int j = blockIdx.x;
+  if (j >= n_jobs) return;
+  JobDev& job = jobs[j];
+  if (!job.scan_fallback) return;
+  Window win{job.data, job.data_len, kFarAway, sh.win};
+  int64_t pos = 0;
+  int np = 0;
+  int status = kOK;
+  bool dict_seen = false;
+  int dict_page = -1;
+  int64_t scratch = 0;
+  int64_t slots = 0;
+  const int lane = lane_id();
+  const int64_t tcs = job.tcs;
+  while (tcs - pos > 0) {
+    Compact<WinSrc> c;
+    c.src.w = win;
+    c.pos = pos;
+    c.frames = sh.frames;
+    c.last = sh.last;
+    c.nlast = 0;
+    c.last_id = 0;
+    c.bool_set = false;
+    c.bool_val = false;
+    PageHdr h;
+    int e = c.read_page_header(&h);
+    win = c.src.w;
+    PageDev pg;
+    init_page(pg, j, pos, c.pos);
+    pg.slot_offset = slots;
+    int64_t next, comp;
+    e = classify_page(job, h, e, c.pos, dict_seen, pg, &next, &comp);
+    if (comp > 0) {
+      pg.scratch_offset = scratch;
+      scratch += comp;
+    }
+    pg.read_status = e;
+    if (np < job.page_cap && lane == 0) pages[job.page_base + np] = pg;
+    if (h.type == 0 || h.type == 3) slots += (e == kOK) ? pg.num_values : 0;
+    if (e == kOK && h.type == 2) {
+      dict_seen = true;
+      dict_page = np;
+    }
+    np++;
+    if (e != kOK) {
+      status = e;
+      break;
+    }
+    pos = next;
+  }
+  if (lane == 0) {
+    init_job_results(job);
+    job.num_pages = np;
+    job.dict_page = dict_page;
+    job.scan_status = status;
+    job.need_scratch = scratch;
+    job.num_slots = slots;
+    if (np > job.page_cap || slots > job.slot_cap || scratch > job.scratch_cap) job.status = kCAPACITY;
+  }
+}
+
+// ============================================================================
+// K1f: compact list of page indices over all jobs.
+// ============================================================================
+__global__ void k_page_list(JobDev* jobs, int n_jobs, int* list, int list_cap, int* total, int* queues) {
+  int off = 0;
+  for (int j = 0; j < n_jobs; j++) {
+    int n = jobs[j].num_pages;
+    if (n > jobs[j].page_cap) n = jobs[j].page_cap;
+    if (jobs[j].status == kCAPACITY) n = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+      if (off + i < list_cap) list[off + i] = (int)(jobs[j].page_base + i);
+    off += n;
+  }
+  if (threadIdx.x == 0) {
+    *total = off < list_cap ? off : list_cap;
+    for (int q = 0; q < 8; q++) queues[q] = 0;
+  }
+}
+
+}  // namespace pqg

@@ -16,6 +16,15 @@
 #pragma once
 #include "pqg_common.h"
 
+// Every method is force-inlined: a parser object whose address escapes into
+// an out-of-line call lives in scratch memory on the GPU, and every byte read
+// then round-trips through it.
+#if defined(__HIPCC__)
+#define PQG_TINLINE __host__ __device__ __attribute__((always_inline)) inline
+#else
+#define PQG_TINLINE inline
+#endif
+
 namespace pqg {
 
 enum : int { T_STOP = 0, T_BOOL = 2, T_BYTE = 3, T_DOUBLE = 4, T_I16 = 6, T_I32 = 8, T_I64 = 10,
@@ -50,14 +59,14 @@ struct Compact {
   int lcap = kMaxLast;
   bool overflow = false;
 
-  __host__ __device__ int byte(uint8_t* b) {
+  PQG_TINLINE int byte(uint8_t* b) {
     int v = src.get(pos);
     if (v < 0) return -1;
     pos++;
     *b = (uint8_t)v;
     return 0;
   }
-  __host__ __device__ int varint64(int64_t* out) {
+  PQG_TINLINE int varint64(int64_t* out) {
     unsigned shift = 0;
     uint64_t r = 0;
     for (;;) {
@@ -70,20 +79,20 @@ struct Compact {
     *out = (int64_t)r;
     return 0;
   }
-  __host__ __device__ int i32(int32_t* out) {
+  PQG_TINLINE int i32(int32_t* out) {
     int64_t v;
     if (varint64(&v)) return -1;
     int32_t n = (int32_t)v;
     *out = (int32_t)((uint32_t)n >> 1) ^ -(n & 1);
     return 0;
   }
-  __host__ __device__ int i64(int64_t* out) {
+  PQG_TINLINE int i64(int64_t* out) {
     int64_t v;
     if (varint64(&v)) return -1;
     *out = (int64_t)((uint64_t)v >> 1) ^ -(v & 1);
     return 0;
   }
-  __host__ __device__ static int ttype(int t) {  // getTType; -1 = unknown
+  PQG_TINLINE static int ttype(int t) {  // getTType; -1 = unknown
     switch (t & 0x0f) {
       case 0: return T_STOP;
       case 1: case 2: return T_BOOL;
@@ -100,7 +109,7 @@ struct Compact {
     }
     return -1;
   }
-  __host__ __device__ int struct_begin() {
+  PQG_TINLINE int struct_begin() {
     if (nlast >= lcap) {
       if (lcap < kMaxLast) overflow = true;
       return -1;
@@ -109,11 +118,11 @@ struct Compact {
     last_id = 0;
     return 0;
   }
-  __host__ __device__ void struct_end() {
+  PQG_TINLINE void struct_end() {
     if (nlast > 0) last_id = last[--nlast];
   }
   // ReadFieldBegin: returns 0 ok / -1 error; *type = T_STOP on error.
-  __host__ __device__ int field_begin(int* type, int* id) {
+  PQG_TINLINE int field_begin(int* type, int* id) {
     *type = T_STOP;
     *id = 0;
     uint8_t t;
@@ -142,7 +151,7 @@ struct Compact {
     *id = fid;
     return 0;
   }
-  __host__ __device__ int read_bool(bool* v) {
+  PQG_TINLINE int read_bool(bool* v) {
     if (bool_set) {
       bool_set = false;
       *v = bool_val;
@@ -153,7 +162,7 @@ struct Compact {
     *v = b == 1;
     return 0;
   }
-  __host__ __device__ int binary_skip() {
+  PQG_TINLINE int binary_skip() {
     int64_t v;
     if (varint64(&v)) return -1;
     int32_t len = (int32_t)v;
@@ -168,7 +177,7 @@ struct Compact {
   }
   // Start processing one value of `type` at `depth`: primitives complete
   // immediately; containers push a frame.  Returns 0 / -1.
-  __host__ __device__ int start_value(int type, int depth, int* nf) {
+  PQG_TINLINE int start_value(int type, int depth, int* nf) {
     if (depth <= 0) return -1;
     switch (type) {
       case T_BOOL: { bool b; return read_bool(&b); }
@@ -233,7 +242,7 @@ struct Compact {
     return -1;  // STOP / unknown: "Unknown data type"
   }
   // protocol.go Skip(fieldType, depth) — iterative.
-  __host__ __device__ int skip(int type, int depth) {
+  PQG_TINLINE int skip(int type, int depth) {
     int nf = 0;
     int e = start_value(type, depth, &nf);
     for (;;) {
@@ -279,7 +288,7 @@ struct Compact {
     }
   }
   // Statistics.Read: binary 1,2,5,6; i64 3,4.
-  __host__ __device__ int read_statistics() {
+  PQG_TINLINE int read_statistics() {
     if (struct_begin()) return -1;
     for (;;) {
       int t, id;
@@ -299,7 +308,7 @@ struct Compact {
     struct_end();
     return 0;
   }
-  __host__ __device__ int read_page_header(PageHdr* h) {
+  PQG_TINLINE int read_page_header(PageHdr* h) {
     int64_t start = pos;
     h->type = h->usize = h->csize = 0;
     h->num_values = h->encoding = h->def_enc = h->rep_enc = 0;
@@ -361,7 +370,7 @@ struct Compact {
     h->hlen = (int32_t)(pos - start);
     return kOK;
   }
-  __host__ __device__ int read_dph(PageHdr* h) {
+  PQG_TINLINE int read_dph(PageHdr* h) {
     if (struct_begin()) return -1;
     bool a = false, b = false, c = false, d = false;
     for (;;) {
@@ -380,7 +389,7 @@ struct Compact {
     struct_end();
     return (a && b && c && d) ? 0 : -1;
   }
-  __host__ __device__ int read_dict(PageHdr* h) {
+  PQG_TINLINE int read_dict(PageHdr* h) {
     if (struct_begin()) return -1;
     bool a = false, b = false;
     for (;;) {
@@ -397,7 +406,7 @@ struct Compact {
     struct_end();
     return (a && b) ? 0 : -1;
   }
-  __host__ __device__ int read_v2(PageHdr* h) {
+  PQG_TINLINE int read_v2(PageHdr* h) {
     if (struct_begin()) return -1;
     unsigned seen = 0;
     for (;;) {

@@ -1,0 +1,477 @@
+// pqg_values.hip — K4: values[:notNull] of every data page, K5: chunk status.
+//
+//   K4 k_values    one wave per data page: valuesDecoder.init (read phase) and
+//                  decodeValues (chunk_reader.go:143-196 dispatch): PLAIN
+//                  fixed-width copies (type_int32.go:12-37, type_int64.go:12-37,
+//                  type_int96.go:21-42, type_float.go:23-33, type_double.go:22-32,
+//                  type_boolean.go:10-69), RLE_DICTIONARY gather through the
+//                  index run table (type_dict.go:39-59), DELTA_BINARY_PACKED
+//                  (deltabp_decoder.go:14-334), RLE booleans
+//   K5 k_finalize  chunk status in reference order
+#include <hip/hip_runtime.h>
+
+#include "pqg_common.h"
+#include "pqg_device.h"
+#include "pqg_hybrid.h"
+
+namespace pqg {
+
+// ============================================================================
+// K4: values — one wave per data page.
+// ============================================================================
+// dictDecoder.decodeValues (type_dict.go:39-59): dst[i] = values[key],
+// "dict: invalid index" when key >= len(values).  W bytes per entry.
+template <int W>
+struct DictSink {
+  uint8_t* out;
+  const uint8_t* dict;
+  int64_t count;
+  int64_t bad;      // first index with an invalid key
+  int64_t nil_key;  // INT96 partial final entry (-1: none): its value reads as zero bytes (Q8)
+  int w;            // entry width when W == 0
+  __device__ __forceinline__ void put(int64_t i0, const uint32_t (&v)[8], int cnt) {
+    bool ok = true;
+    for (int q = 0; q < cnt; q++)
+      if ((int64_t)v[q] >= count) {
+        ok = false;
+        bad = i0 + q < bad ? i0 + q : bad;
+      }
+    if (W == 4 && ok && cnt == 8 && ((uintptr_t)(out + i0 * 4) & 15) == 0) {
+      const uint32_t* d = (const uint32_t*)dict;
+      uint4 a = make_uint4(d[v[0]], d[v[1]], d[v[2]], d[v[3]]);
+      uint4 b = make_uint4(d[v[4]], d[v[5]], d[v[6]], d[v[7]]);
+      uint4* o = (uint4*)(out + i0 * 4);
+      o[0] = a;
+      o[1] = b;
+      return;
+    }
+    if (W == 8 && ok && cnt == 8 && ((uintptr_t)(out + i0 * 8) & 15) == 0) {
+      const uint2* d = (const uint2*)dict;
+      uint4* o = (uint4*)(out + i0 * 8);
+#pragma unroll
+      for (int q = 0; q < 8; q += 2) {
+        const uint2 x = d[v[q]], y = d[v[q + 1]];
+        o[q / 2] = make_uint4(x.x, x.y, y.x, y.y);
+      }
+      return;
+    }
+    const int ww = W > 0 ? W : w;
+    for (int q = 0; q < cnt; q++) {
+      const int64_t key = v[q];
+      if (key >= count) continue;
+      const int64_t i = i0 + q;
+      if (W == 4) {
+        *(uint32_t*)(out + i * 4) = *(const uint32_t*)(dict + key * 4);
+      } else if (W == 8) {
+        const uint32_t* s = (const uint32_t*)(dict + key * 8);
+        uint32_t* d = (uint32_t*)(out + i * 8);
+        d[0] = s[0];
+        d[1] = s[1];
+      } else {
+        const uint8_t* s = dict + key * ww;
+        for (int b = 0; b < ww; b++) out[i * ww + b] = (key == nil_key) ? 0 : s[b];
+      }
+    }
+  }
+};
+
+// booleanRLEDecoder (type_boolean.go:100-120): value == 1
+struct BoolSink {
+  uint8_t* out;
+  __device__ __forceinline__ void put(int64_t i0, const uint32_t (&v)[8], int cnt) {
+    for (int q = 0; q < cnt; q++) out[i0 + q] = v[q] == 1;
+  }
+};
+
+// ---- DELTA_BINARY_PACKED (deltabp_decoder.go) ------------------------------
+constexpr int kBlocks = 64;
+constexpr int kMaxMb = 8;
+
+struct DbpShared {
+  uint8_t win[kWin];
+  int64_t body[kBlocks];                // stream offset of the block's first miniblock
+  uint64_t mind[kBlocks];               // min delta (as unsigned for wrapping adds)
+  uint8_t widths[kBlocks][kMaxMb];
+  int64_t mb_off[kBlocks][kMaxMb];      // stream offset of each miniblock
+};
+
+__device__ __forceinline__ int read_uvarint64(Window& w, int64_t& pos, uint64_t* out) {
+  uint64_t x = 0;
+  unsigned s = 0;
+  for (int i = 0;; i++) {
+    int b = w.get(pos);
+    if (b < 0) return kEOF;
+    pos++;
+    if (b < 0x80) {
+      if (i > 9 || (i == 9 && b > 1)) return kRLE;
+      *out = x | (s < 64 ? (uint64_t)b << s : 0);
+      return kOK;
+    }
+    if (s < 64) x |= (uint64_t)(b & 0x7f) << s;
+    s += 7;
+  }
+}
+// readVariant32 / readVariant64 with the oracle's error classes
+__device__ __forceinline__ int read_signed(Window& w, int64_t& pos, bool is64, uint64_t* out) {
+  uint64_t ux;
+  int e = read_uvarint64(w, pos, &ux);
+  if (e) return e == kEOF ? kEOF : kDELTA;
+  int64_t x = (int64_t)(ux >> 1);
+  if (ux & 1) x = ~x;
+  if (!is64 && (x > 2147483647LL || x < -2147483648LL)) return kDELTA;
+  *out = (uint64_t)x;
+  return kOK;
+}
+__device__ __forceinline__ int read_u32var_delta(Window& w, int64_t& pos, int32_t* out) {
+  uint64_t v;
+  int e = read_uvarint64(w, pos, &v);
+  if (e) return e == kEOF ? kEOF : kDELTA;
+  if (v > 0x7fffffffull) return kDELTA;
+  *out = (int32_t)v;
+  return kOK;
+}
+
+// Values of a DBP page: emulates deltaBitPackDecoder{32,64}.next for positions
+// [0, nn).  Regular layout (miniblock value count a multiple of 8, <= kMaxMb
+// miniblocks): wave-parallel unpack + wrapping scan; otherwise one lane.
+__device__ int dbp_decode(const uint8_t* s, int64_t n, int64_t readable, bool is64, int64_t nn, uint8_t* out,
+                          DbpShared& sh, int stage /*0 = header only (read phase), 1 = decode*/) {
+  const int lane = lane_id();
+  Window win{s, n, kFarAway, sh.win};
+  int64_t pos = 0;
+  int32_t bs, mbc, total;
+  uint64_t first;
+  int e;
+  // readBlockHeader
+  if ((e = read_u32var_delta(win, pos, &bs))) return e;
+  if (bs <= 0 && bs % 128 != 0) return kDELTA;
+  if ((e = read_u32var_delta(win, pos, &mbc))) return e;
+  if (mbc <= 0 || bs % mbc != 0) return kDELTA;
+  int32_t mbvc = bs / mbc;
+  if (mbvc == 0) return kDELTA;
+  if ((e = read_u32var_delta(win, pos, &total))) return e;
+  if ((e = read_signed(win, pos, is64, &first))) return e;
+  const int maxw = is64 ? 64 : 32;
+  // first readMiniBlockHeader (part of init)
+  {
+    int64_t p = pos;
+    uint64_t md;
+    if ((e = read_signed(win, p, is64, &md))) return e;
+    if (n - p < mbc) return kEOF;
+    for (int m = 0; m < mbc; m++)
+      if (win.get(p + m) > maxw) return kBIT_WIDTH;
+  }
+  if (stage == 0) return kOK;
+  const int64_t P = nn < total ? nn : total;  // positions actually produced before EOF
+  const bool regular = (mbvc % 8 == 0) && mbc <= kMaxMb;
+  if (!regular) {
+    // ---- generic single-lane emulation of next() (rare layouts)
+    int64_t rp = pos;
+    int32_t cur_mb = mbc;  // force header read at position 0 semantics below
+    uint64_t mind = 0, prev = first;
+    uint8_t widths[256];
+    int32_t cw = 0, mbpos = 0;
+    uint64_t vals[8] = {0};
+    // init already read the first miniblock header: emulate it
+    {
+      if ((e = read_signed(win, rp, is64, &mind))) return e;
+      for (int m = 0; m < mbc && m < 256; m++) widths[m] = (uint8_t)win.get(rp + m);
+      if (mbc > 256) return kUNSUPPORTED;
+      rp += mbc;
+      cur_mb = 0;
+    }
+    for (int64_t p = 0; p < nn; p++) {
+      if (p >= total) return kEOF;
+      if (p % 8 == 0) {
+        if (p % mbvc == 0) {
+          if (cur_mb >= mbc) {
+            if ((e = read_signed(win, rp, is64, &mind))) return e;
+            if (n - rp < mbc) return kEOF;
+            for (int m = 0; m < mbc; m++) {
+              int wv = win.get(rp + m);
+              if (wv > maxw) return kBIT_WIDTH;
+              widths[m] = (uint8_t)wv;
+            }
+            rp += mbc;
+            cur_mb = 0;
+          }
+          cw = widths[cur_mb];
+          mbpos = 0;
+          cur_mb++;
+        }
+        if (n - rp < cw) return kEOF;
+        for (int k = 0; k < 8; k++) vals[k] = extract_bits64(s, readable, n, rp * 8 + (int64_t)k * cw, cw);
+        rp += cw;
+        mbpos += cw;
+        if (p + 8 >= total) {
+          int64_t l = (int64_t)(mbvc / 8) * cw - mbpos;
+          if (l < 0) return kDELTA;
+          rp += l;  // padding skip, errors ignored
+          if (rp > n) rp = n;
+        }
+      }
+      if (lane == 0) {
+        if (is64) *(uint64_t*)(out + p * 8) = prev;
+        else *(uint32_t*)(out + p * 4) = (uint32_t)prev;
+      }
+      prev = prev + vals[p % 8] + mind;
+      if (!is64) prev = (uint32_t)prev;
+    }
+    return kOK;
+  }
+  // ---- regular layout: walk blocks in batches, then unpack + scan
+  uint64_t carry = first;  // value at the first position of the next tile
+  int64_t blk_pos = pos;   // stream offset of the next block header
+  int64_t p0 = 0;          // first position of the current batch
+  bool first_block = true;
+  while (p0 < P) {
+    int nb = 0;
+    int64_t p_end = p0;
+    while (nb < kBlocks && p_end < P) {
+      // block header: min delta + widths (the first one was read by init)
+      int64_t hp = blk_pos;
+      uint64_t md;
+      if ((e = read_signed(win, hp, is64, &md))) return e;
+      if (n - hp < mbc) return kEOF;
+      int64_t off = hp + mbc;
+      for (int m = 0; m < mbc; m++) {
+        int wv = win.get(hp + m);
+        if (wv > maxw) return kBIT_WIDTH;
+        if (lane == 0) {
+          sh.widths[nb][m] = (uint8_t)wv;
+          sh.mb_off[nb][m] = off;
+        }
+        off += (int64_t)(mbvc / 8) * wv;
+      }
+      // groups of this block that positions < P read: each must be whole
+      int64_t bp0 = p_end;
+      int64_t bp1 = bp0 + bs < P ? bp0 + bs : P;
+      int64_t last_group_pos = ((bp1 - 1) / 8) * 8;   // position of the last group read
+      int64_t rel = last_group_pos - bp0;
+      int m_last = (int)(rel / mbvc);
+      int64_t g_in_mb = (rel % mbvc) / 8;
+      int wl = win.get(hp + m_last);
+      int64_t g_end = 0;
+      {
+        // offset of the last group's end
+        int64_t mo = hp + mbc;
+        for (int m = 0; m < m_last; m++) mo += (int64_t)(mbvc / 8) * win.get(hp + m);
+        g_end = mo + (g_in_mb + 1) * wl;
+      }
+      if (g_end > n) return kEOF;
+      if (lane == 0) {
+        sh.body[nb] = hp + mbc;
+        sh.mind[nb] = md;
+      }
+      nb++;
+      p_end = bp1;
+      blk_pos = off;
+      first_block = false;
+    }
+    (void)first_block;
+    __builtin_amdgcn_wave_barrier();
+    // unpack + wrapping prefix over positions [p0, p_end): value(p) = carry + Σ deltas
+    for (int64_t t0 = p0; t0 < p_end; t0 += 256) {
+      uint64_t d[4];
+      uint64_t local = 0;
+      for (int k = 0; k < 4; k++) {
+        int64_t p = t0 + lane * 4 + k;
+        uint64_t dv = 0;
+        if (p < p_end) {
+          int64_t rel = p - p0;
+          int b = (int)(rel / bs);
+          int64_t r2 = rel - (int64_t)b * bs;
+          int m = (int)(r2 / mbvc);
+          int64_t j = r2 - (int64_t)m * mbvc;
+          int wv = sh.widths[b][m];
+          uint64_t x = extract_bits64(s, readable, n, sh.mb_off[b][m] * 8 + j * wv, wv);
+          dv = x + sh.mind[b];
+        }
+        d[k] = dv;
+        local += dv;
+      }
+      uint64_t incl = wave_incl_scan_u64(local);
+      uint64_t run = carry + (incl - local);
+      for (int k = 0; k < 4; k++) {
+        int64_t p = t0 + lane * 4 + k;
+        if (p < p_end) {
+          if (is64) *(uint64_t*)(out + p * 8) = run;
+          else *(uint32_t*)(out + p * 4) = (uint32_t)run;
+        }
+        run += d[k];
+      }
+      carry += __shfl(incl, 63, 64);
+    }
+    __builtin_amdgcn_wave_barrier();
+    p0 = p_end;
+  }
+  if (nn > total) return kEOF;
+  return kOK;
+}
+
+union ValuesShared {
+  ExpandShared ex;
+  DbpShared dbp;
+};
+
+__global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+                                               int* queue, uint8_t* value_arena, const HStream* streams,
+                                               const RunEnt* runs, const int32_t* blks) {
+  __shared__ __attribute__((aligned(16))) ValuesShared sh;
+  const int lane = lane_id();
+  for (;;) {
+    int t = 0;
+    if (lane == 0) t = atomicAdd(queue, 1);
+    t = __shfl(t, 0, 64);
+    if (t >= *total) return;
+    PageDev& pg = pages[list[t]];
+    if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3)) continue;
+    JobDev& job = jobs[pg.job];
+    if (job.status == kCAPACITY) continue;
+    const uint8_t* val = pg.val;
+    const int64_t vn = pg.val_n;
+    // readable bytes from val (for wide loads)
+    int64_t readable = (pg.scratch_offset >= 0) ? vn : job.data_len - (val - job.data);
+    const int enc = pg.encoding;
+    const int64_t nn = pg.not_null;
+    const int w = job.value_width;
+    uint8_t* out = value_arena + job.value_base + pg.value_offset * (int64_t)w;
+    // ---- valuesDecoder.init (read phase)
+    int re = kOK;
+    int dict_w = 0;
+    if (enc == 8) {
+      if (vn < 1) re = kEOF;
+      else {
+        dict_w = val[0];
+        if (dict_w > 32) re = kBIT_WIDTH;
+      }
+    } else if (enc == 5) {
+      re = dbp_decode(val, vn, readable, job.type == 2, 0, nullptr, sh.dbp, 0);
+    } else if (enc == 3 && job.type == 0) {
+      if (vn < 4) re = kEOF;
+    }
+    if (re != kOK) {
+      if (lane == 0) pg.read_status = re;
+      continue;
+    }
+    if (pg.decode_status != kOK || nn == 0) continue;
+    // ---- decodeValues(val[:nn]) (decode phase)
+    int de = kOK;
+    if (enc == 0) {
+      if (job.type == 0) {  // booleanPlainDecoder: one byte per 8 values
+        if ((nn + 7) / 8 > vn) de = kEOF;
+        else
+          for (int64_t i = lane; i < nn; i += 64) out[i] = (val[i >> 3] >> (i & 7)) & 1;
+      } else if (job.type == 3) {  // INT96 (type_int96.go:21-42)
+        int64_t full = vn / 12, rem = vn % 12;
+        if (nn > full + (rem > 0 ? 1 : 0)) de = kEOF;
+        else {
+          if (nn == full + 1 && rem > 0 && lane == 0) pg.flags |= 1;
+          for (int64_t i = lane; i < nn * 12; i += 64) out[i] = (i < full * 12) ? val[i] : 0;
+        }
+      } else if (w > 0 && (w & 3) != 0) {  // FLBA of odd length: byte copy
+        if (nn * w > vn) de = kEOF;
+        else
+          for (int64_t i = lane; i < nn * w; i += 64) out[i] = val[i];
+      } else if (w > 0) {
+        if (nn * w > vn) de = kEOF;
+        else {
+          int64_t nb = nn * w;
+          // 16-byte destination chunks; source may be unaligned
+          for (int64_t i = (int64_t)lane * 4; i < nb; i += 256) {
+            if (i + 4 <= nb) {
+              uint64_t x = load_u64_masked(val, readable, i, vn);
+              *(uint32_t*)(out + i) = (uint32_t)x;
+            } else {
+              for (int64_t b = i; b < nb; b++) out[b] = val[b];
+            }
+          }
+        }
+      } else {
+        de = kUNSUPPORTED;  // PLAIN byte arrays: not in this build yet
+      }
+    } else if (enc == 8) {
+      const uint8_t* dict = job.dict_data;
+      const int64_t dcount = job.dict_data ? job.dict_count : 0;
+      const int64_t nil_key = (job.flags & 1) ? dcount - 1 : -1;
+      if (w == 0) {
+        de = kUNSUPPORTED;  // variable-length dictionaries: not in this build yet
+      } else if (dict_w == 0) {
+        // a zero-width decoder yields key 0 forever, reading nothing (hybrid_decoder.go:84-86)
+        if (dcount < 1) de = kDICT_INDEX;
+        else
+          for (int64_t b = lane; b < nn * w; b += 64) out[b] = (0 == nil_key) ? 0 : dict[b % w];
+      } else {
+        const HStream& S = streams[pg.hs_val];
+        const int serr = (S.status != kOK && S.produced < nn) ? S.status : kOK;
+        int64_t bad = nn;
+        if (w == 4) {
+          DictSink<4> sk{out, dict, dcount, nn, nil_key, 4};
+          hybrid_expand(S, runs, blks, nn, sh.ex, sk);
+          bad = wave_min(sk.bad);
+        } else if (w == 8) {
+          DictSink<8> sk{out, dict, dcount, nn, nil_key, 8};
+          hybrid_expand(S, runs, blks, nn, sh.ex, sk);
+          bad = wave_min(sk.bad);
+        } else {
+          DictSink<0> sk{out, dict, dcount, nn, nil_key, w};
+          hybrid_expand(S, runs, blks, nn, sh.ex, sk);
+          bad = wave_min(sk.bad);
+        }
+        if (bad < nn && (serr == kOK || bad < S.produced)) de = kDICT_INDEX;
+        else de = serr;
+      }
+    } else if (enc == 5) {
+      de = dbp_decode(val, vn, readable, job.type == 2, nn, out, sh.dbp, 1);
+    } else if (enc == 3 && job.type == 0) {  // booleanRLEDecoder: hybrid w=1 after a u32 length
+      const HStream& S = streams[pg.hs_val];
+      BoolSink sk{out};
+      hybrid_expand(S, runs, blks, nn, sh.ex, sk);
+      de = (S.status != kOK && S.produced < nn) ? S.status : kOK;
+    } else {
+      de = kUNSUPPORTED;
+    }
+    if (lane == 0 && de != kOK) pg.decode_status = de;
+  }
+}
+
+// ============================================================================
+// K5: chunk status in reference order (readPages errors first, then
+// readPageData errors) — one 256-lane block per job, min-reductions over pages.
+// ============================================================================
+__global__ void __launch_bounds__(256) k_finalize(JobDev* jobs, int n_jobs, PageDev* pages) {
+  __shared__ int s_read, s_dec;
+  JobDev& job = jobs[blockIdx.x];
+  if (job.status == kCAPACITY) return;
+  const int np = job.num_pages < job.page_cap ? job.num_pages : job.page_cap;
+  if (threadIdx.x == 0) {
+    s_read = INT32_MAX;
+    s_dec = INT32_MAX;
+  }
+  __syncthreads();
+  const PageDev* pg = pages + job.page_base;
+  int r = INT32_MAX, d = INT32_MAX;
+  for (int i = threadIdx.x; i < np; i += 256) {
+    if (pg[i].read_status != kOK && i < r) r = i;
+    if ((pg[i].page_type == 0 || pg[i].page_type == 3) && pg[i].decode_status != kOK && i < d) d = i;
+  }
+  if (r != INT32_MAX) atomicMin(&s_read, r);
+  if (d != INT32_MAX) atomicMin(&s_dec, d);
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  int status = kOK, ep = -1;
+  if (s_read != INT32_MAX) {
+    ep = s_read;
+    status = pg[ep].read_status;
+  }
+  job.n_out_pages = ep >= 0 ? ep + 1 : np;
+  if (status == kOK && s_dec != INT32_MAX) {
+    ep = s_dec;
+    status = pg[ep].decode_status;
+  }
+  job.status = status;
+  job.error_page = ep;
+}
+
+}  // namespace pqg
+
