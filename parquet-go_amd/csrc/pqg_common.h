@@ -79,7 +79,7 @@ struct HStream {
   const uint8_t* p;  // first byte of the stream
   int64_t n;         // stream bytes (reads at or past n are EOF)
   int64_t run_base;  // first RunEnt of the stream's run table
-  int64_t blk_base;  // first entry of its block index (run of value k*kHBlock)
+  int64_t blk_base;  // first BlockDesc of the stream
   int32_t page;      // PageDev index
   int32_t kind;      // 0 rep, 1 def, 2 dictionary indices, 3 RLE booleans
   int32_t w;         // bit width (1..32)
@@ -88,7 +88,17 @@ struct HStream {
   int32_t n_runs;
   int32_t produced;  // values available before the end of the stream / an error
   int32_t status;    // error met after `produced` values (kOK: none before `count`)
-  int32_t pad;
+  int32_t n_blocks;  // BlockDescs written
+};
+
+// A block of a stream's values for the expanders: at most kHBlock values and
+// kHBlockRuns runs, with the byte range of the bit-packed payload they use.
+struct BlockDesc {
+  uint32_t v0;      // first value index
+  uint32_t r0;      // first run (index into the stream's run table)
+  uint32_t lo;      // first payload byte used (stream offset)
+  uint16_t nbytes;  // payload bytes used from lo (0: RLE only)
+  uint16_t nr;      // runs in the block
 };
 
 // Run table entry: start = first value index of the run (bit 31: bit-packed);
@@ -98,7 +108,8 @@ struct RunEnt {
   uint32_t src;
 };
 constexpr uint32_t kRunBP = 0x80000000u;
-constexpr int kHBlock = 512;  // values per block of the block index / expander step
+constexpr int kHBlock = 512;      // values per expander block
+constexpr int kHBlockRuns = 64;   // runs per expander block (one per lane)
 
 struct JobDev {
   // ---- inputs

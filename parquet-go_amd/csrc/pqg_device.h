@@ -4,7 +4,45 @@
 
 #include "pqg_common.h"
 
+// Address-space typed pointers.  Pointers loaded from memory (JobDev.data,
+// HStream.p, ...) are generic to the compiler, and generic accesses become
+// FLAT instructions, which count in both vmcnt and lgkmcnt: every LDS wait then
+// also waits for all outstanding global loads and stores.  Hot code therefore
+// converts them to global (address space 1) once, at the load of the pointer.
+#define PQG_G __attribute__((address_space(1)))
+#define PQG_L __attribute__((address_space(3)))
+
 namespace pqg {
+
+typedef const PQG_G uint8_t* gcu8;
+typedef PQG_G uint8_t* gu8;
+template <class T>
+__device__ __forceinline__ const PQG_G T* gconst(const T* p) { return (const PQG_G T*)p; }
+template <class T>
+__device__ __forceinline__ PQG_G T* gmut(T* p) { return (PQG_G T*)p; }
+template <class T>
+__device__ __forceinline__ PQG_L T* lds_ptr(T* p) { return (PQG_L T*)p; }
+
+// 16 / 8-byte global and LDS accesses (HIP's uint4 class does not copy out of
+// an address-space-qualified lvalue, a clang vector type does).
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ldg16(uintptr_t a) {
+  const u32x4_t v = *(const PQG_G u32x4_t*)a;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void stg16(uintptr_t a, uint4 x) {
+  const u32x4_t v = {x.x, x.y, x.z, x.w};
+  *(PQG_G u32x4_t*)a = v;
+}
+__device__ __forceinline__ void stg8(uintptr_t a, uint32_t lo, uint32_t hi) {
+  const u32x2_t v = {lo, hi};
+  *(PQG_G u32x2_t*)a = v;
+}
+__device__ __forceinline__ void sts16(PQG_L void* a, uint4 x) {
+  const u32x4_t v = {x.x, x.y, x.z, x.w};
+  *(PQG_L u32x4_t*)a = v;
+}
 
 constexpr int kWave = 64;
 
@@ -24,19 +62,20 @@ __device__ __forceinline__ int values_supported(int type, int type_length, int e
   return 0;
 }
 
-__device__ __forceinline__ uint32_t rd_u32(const uint8_t* p) {
+template <class P>
+__device__ __forceinline__ uint32_t rd_u32(P p) {
   return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
 }
 
 // One lane's byte reader over [p, p+n): 16-byte granules cached in registers
 // (a granule holding a byte < n lies in mapped memory).  -1 past the end.
 struct LaneBytes {
-  const uint8_t* p;
+  gcu8 p;
   int64_t n;
   uintptr_t gaddr;
   uint4 g;
   __device__ __forceinline__ void init(const uint8_t* p_, int64_t n_) {
-    p = p_;
+    p = gconst(p_);
     n = n_;
     gaddr = 0;
   }
@@ -45,7 +84,7 @@ struct LaneBytes {
     const uintptr_t a = (uintptr_t)(p + i);
     const uintptr_t ga = a & ~(uintptr_t)15;
     if (ga != gaddr) {
-      g = *(const uint4*)ga;
+      g = ldg16(ga);
       gaddr = ga;
     }
     const int w = (int)((a >> 2) & 3);
@@ -55,7 +94,8 @@ struct LaneBytes {
 };
 
 // Bounds-checked byte read of a device buffer.
-__device__ __forceinline__ int get_byte(const uint8_t* p, int64_t n, int64_t i) {
+template <class P>
+__device__ __forceinline__ int get_byte(P p, int64_t n, int64_t i) {
   return (i >= 0 && i < n) ? (int)p[i] : -1;
 }
 
@@ -63,11 +103,12 @@ __device__ __forceinline__ int get_byte(const uint8_t* p, int64_t n, int64_t i) 
 // beyond `valid` read as 0 (Q5 zero padding), bytes beyond n are never touched.
 // Fast path: the aligned dwords covering [i, i+8) all contain a readable byte,
 // so they lie on pages that are mapped.
-__device__ __forceinline__ uint64_t load_u64_masked(const uint8_t* p, int64_t n, int64_t i, int64_t valid) {
+template <class P>
+__device__ __forceinline__ uint64_t load_u64_masked(P p, int64_t n, int64_t i, int64_t valid) {
   int64_t lim = valid < n ? valid : n;
   if (i >= 0 && i + 8 <= lim) {
     uintptr_t a = (uintptr_t)(p + i);
-    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+    const PQG_G uint32_t* q = (const PQG_G uint32_t*)(a & ~(uintptr_t)3);
     int sh = (int)(a & 3) * 8;
     uint64_t lo = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
     if (sh == 0) return lo;
@@ -83,7 +124,8 @@ __device__ __forceinline__ uint64_t load_u64_masked(const uint8_t* p, int64_t n,
 }
 
 // Extract `w` (<= 32) bits at bit offset `bit` of stream [p, p+valid).
-__device__ __forceinline__ uint32_t extract_bits32(const uint8_t* p, int64_t n, int64_t valid, int64_t bit, int w) {
+template <class P>
+__device__ __forceinline__ uint32_t extract_bits32(P p, int64_t n, int64_t valid, int64_t bit, int w) {
   if (w == 0) return 0;
   uint64_t x = load_u64_masked(p, n, bit >> 3, valid);
   x >>= (bit & 7);
@@ -91,7 +133,8 @@ __device__ __forceinline__ uint32_t extract_bits32(const uint8_t* p, int64_t n, 
 }
 
 // Extract `w` (<= 64) bits.
-__device__ __forceinline__ uint64_t extract_bits64(const uint8_t* p, int64_t n, int64_t valid, int64_t bit, int w) {
+template <class P>
+__device__ __forceinline__ uint64_t extract_bits64(P p, int64_t n, int64_t valid, int64_t bit, int w) {
   if (w == 0) return 0;
   int64_t byte = bit >> 3;
   int sh = (int)(bit & 7);
@@ -102,6 +145,15 @@ __device__ __forceinline__ uint64_t extract_bits64(const uint8_t* p, int64_t n, 
     v |= hi << (64 - sh);
   }
   return w == 64 ? v : (v & ((1ull << w) - 1));
+}
+
+// Next item of an atomic work queue, wave-uniform (in an SGPR): struct loads
+// indexed by it become scalar loads, which do not queue behind vector loads
+// and stores (vmcnt) the way vector loads of the same fields would.
+__device__ __forceinline__ int queue_next(int* queue) {
+  int t = 0;
+  if (lane_id() == 0) t = atomicAdd(queue, 1);
+  return __builtin_amdgcn_readfirstlane(t);
 }
 
 // ---------------------------------------------------------------------------
@@ -170,10 +222,10 @@ constexpr int kWin = 1024;
 constexpr int64_t kFarAway = -((int64_t)1 << 62);
 
 struct Window {
-  const uint8_t* p;
+  gcu8 p;
   int64_t n;        // readable bytes of the stream
   int64_t base;     // stream offset of window[0]
-  uint8_t* lds;     // kWin bytes (16-byte aligned)
+  PQG_L uint8_t* lds;  // kWin bytes (16-byte aligned)
 
   __device__ void fill(int64_t at) {
     // align the window to 16 bytes of absolute address so each lane moves one
@@ -185,7 +237,7 @@ struct Window {
     int64_t off = base + l * 16;
     uint4 v;
     if (off >= 0 && off + 16 <= n) {
-      v = *(const uint4*)(p + off);
+      v = ldg16((uintptr_t)(p + off));
     } else {
       uint32_t w[4] = {0, 0, 0, 0};
       for (int k = 0; k < 16; k++) {
@@ -194,7 +246,7 @@ struct Window {
       }
       v = make_uint4(w[0], w[1], w[2], w[3]);
     }
-    *(uint4*)(lds + l * 16) = v;
+    sts16(lds + l * 16, v);
     __builtin_amdgcn_wave_barrier();
   }
   // byte at stream offset i, or -1 past the end

@@ -1,136 +1,204 @@
 // pqg_hybrid.h — expansion of RLE / bit-packed hybrid run tables (wave level).
 //
 // k_hybrid_walk (pqg_levels.hip) turns every hybrid stream into a run table
-// (RunEnt) plus a block index (run holding value k*kHBlock).  An expander
-// wave takes a stream one block of kHBlock values at a time: the block's runs
-// and the bit-packed payload bytes they cover are staged in LDS, then every
-// lane produces 8 consecutive values and hands them to a sink (level bytes,
-// dictionary gather, booleans).  Values are exactly hybridDecoder.next's
-// (hybrid_decoder.go:82-166): RLE runs repeat their value, bit-packed runs
-// are LSB-first w-bit fields (unpack8int32_w, bitbacking32.go), bytes past
-// the end of the stream read as zero (the short-read zero padding, Q5).
+// (RunEnt) and block descriptors (BlockDesc: <= kHBlock values, <= kHBlockRuns
+// runs, and the byte range of the bit-packed payload those values use).  An
+// expander wave takes a stream one block at a time: the block's runs and
+// payload bytes are staged in LDS, then every lane produces 8 consecutive
+// values and hands them to a sink (level bytes, dictionary gather, booleans).
+//
+// The loads of block k+1 are issued before block k's sink runs.  vmcnt
+// retires loads and stores in issue order, so a load issued after block k's
+// stores would make its wait cover those stores too; issued before them, it
+// overlaps with block k's gathers and stores.  The two register sets
+// alternate in a 2x unrolled loop, so no in-flight register is copied at the
+// loop latch (a copy would force a full vmcnt(0) wait there).
+//
+// Values are exactly hybridDecoder.next's (hybrid_decoder.go:82-166): RLE runs
+// repeat their value; bit-packed runs are LSB-first w-bit fields
+// (unpack8int32_w, bitbacking32.go); bytes past the end of the stream read as
+// zero (the short-read zero padding, Q5).
 #pragma once
 #include "pqg_device.h"
 
 namespace pqg {
 
-constexpr int kStageBytes = 4096;  // staged payload bytes per block
+constexpr int kStageGranules = 192;  // 16-byte payload granules per block (3 per lane)
 
 struct ExpandShared {
-  RunEnt runs[kHBlock + 2];
-  uint32_t stage[kStageBytes / 4 + 2];
+  BlockDesc desc[64];
+  RunEnt runs[kHBlockRuns];
+  uint32_t stage[kStageGranules * 4 + 4];
 };
 
 __device__ __forceinline__ uint32_t run_start(const RunEnt& r) { return r.start & ~kRunBP; }
 
-// Global-memory fallback: w bits at stream bit `bit`, zero past n.
-__device__ __forceinline__ uint32_t extract_global(const uint8_t* p, int64_t n, int64_t bit, int w) {
-  int64_t byte = bit >> 3;
-  uint64_t x = 0;
-  for (int k = 0; k < 5; k++) {
-    int64_t j = byte + k;
-    if (j < n) x |= (uint64_t)p[j] << (8 * k);
-  }
-  x >>= (bit & 7);
-  return (uint32_t)(x & (w == 32 ? 0xffffffffull : ((1ull << w) - 1)));
+// One block's loads, held in registers between issue and install.
+struct BlockRegs {
+  uint32_t rs, rv;   // this lane's run entry
+  uint4 g0, g1, g2;  // this lane's payload granules (lane, lane+64, lane+128)
+};
+
+struct BlockGeom {
+  uint32_t v0, v1;  // values [v0, v1)
+  uint32_t r0, nr;
+  int64_t sb;       // stream offset of stage byte 0 (a 16-byte aligned address)
+  int ng;           // granules staged
+};
+
+// Block k of the batch in sh.desc[0, nb); `end` bounds the last block.
+__device__ __forceinline__ BlockGeom block_geom(const ExpandShared& sh, int k, int nb, uint32_t end,
+                                                const HStream& S) {
+  BlockGeom g;
+  const BlockDesc& d = sh.desc[k];
+  g.v0 = d.v0;
+  g.v1 = k + 1 < nb ? sh.desc[k + 1].v0 : end;
+  if (g.v1 > end) g.v1 = end;
+  g.r0 = d.r0;
+  g.nr = d.nr;
+  const int64_t lo = d.lo;
+  g.sb = lo - (int64_t)(((uintptr_t)S.p + (uintptr_t)lo) & 15);
+  g.ng = d.nbytes ? (int)((lo + d.nbytes - g.sb + 15) >> 4) + 1 : 0;  // +1: the dword pair read past the end
+  if (g.ng > kStageGranules) g.ng = kStageGranules;
+  return g;
 }
 
-// Sink: void put(int64_t i0, const uint32_t (&v)[8], int cnt)  (cnt <= 8 values from i0)
+// The prefetch loads are unconditional: a load guarded by a branch is merged
+// with the register's old value at the join, and that copy waits (vmcnt) for
+// the load at once.  Lanes with nothing to load read a safe mapped address
+// (`safe`) and block_process ignores the value.
+__device__ __forceinline__ uintptr_t stage_addr(gcu8 sp, int64_t n, int64_t at, bool want, uintptr_t safe) {
+  // a granule holding a stream byte < n is mapped
+  return (want && at < n && at + 16 > 0) ? (uintptr_t)(sp + at) : safe;
+}
+
+__device__ __forceinline__ void block_fetch(BlockRegs& R, const BlockGeom& g, const PQG_G RunEnt* runs, gcu8 sp,
+                                            int64_t n, int lane) {
+  const uint32_t ri = (uint32_t)lane < g.nr ? (uint32_t)lane : 0u;  // nr >= 1
+  R.rs = runs[g.r0 + ri].start;
+  R.rv = runs[g.r0 + ri].src;
+  const uintptr_t safe = (uintptr_t)(runs + g.r0) & ~(uintptr_t)15;
+  R.g0 = ldg16(stage_addr(sp, n, g.sb + 16 * lane, lane < g.ng, safe));
+  R.g1 = ldg16(stage_addr(sp, n, g.sb + 16 * (lane + 64), lane + 64 < g.ng, safe));
+  R.g2 = ldg16(stage_addr(sp, n, g.sb + 16 * (lane + 128), lane + 128 < g.ng, safe));
+}
+
+// zero the bytes of a staged granule at or past the stream end (Q5)
+__device__ __forceinline__ uint4 mask_tail(uint4 v, int64_t at, int64_t n) {
+  if (at + 16 <= n) return v;
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    const int64_t b = at + 4 * d;
+    if (b >= n) w[d] = 0;
+    else if (b + 4 > n) w[d] &= 0xffffffffu >> (8 * (4 - (n - b)));
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 template <class Sink>
-__device__ void hybrid_expand(const HStream& S, const RunEnt* __restrict__ runs, const int32_t* __restrict__ blks,
+__device__ __forceinline__ void block_process(const BlockRegs& R, const BlockGeom& g, ExpandShared& sh,
+                                              const HStream& S, uint32_t mask, int w, int lane, Sink& sink) {
+  __builtin_amdgcn_wave_barrier();
+  if ((uint32_t)lane < g.nr) {
+    sh.runs[lane].start = R.rs;
+    sh.runs[lane].src = R.rv;
+  }
+  PQG_L uint32_t* st = lds_ptr(sh.stage);
+  if (lane < g.ng) sts16(st + 4 * lane, mask_tail(R.g0, g.sb + 16 * lane, S.n));
+  if (lane + 64 < g.ng) sts16(st + 4 * (lane + 64), mask_tail(R.g1, g.sb + 16 * (lane + 64), S.n));
+  if (lane + 128 < g.ng) sts16(st + 4 * (lane + 128), mask_tail(R.g2, g.sb + 16 * (lane + 128), S.n));
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t i0 = g.v0 + lane * 8;
+  if (i0 < g.v1) {
+    const int cnt = (int)(g.v1 - i0 < 8 ? g.v1 - i0 : 8);
+    int lo = 0, hi = (int)g.nr - 1;  // last run with start <= i0
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (run_start(sh.runs[mid]) <= i0) lo = mid; else hi = mid - 1;
+    }
+    int r = lo;
+    RunEnt cur = sh.runs[r];
+    uint32_t nxt = r + 1 < (int)g.nr ? run_start(sh.runs[r + 1]) : 0xffffffffu;
+    uint32_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const uint32_t i = i0 + q;
+      v[q] = 0;
+      if (q < cnt) {
+        while (i >= nxt) {
+          r++;
+          cur = sh.runs[r];
+          nxt = r + 1 < (int)g.nr ? run_start(sh.runs[r + 1]) : 0xffffffffu;
+        }
+        if (!(cur.start & kRunBP)) {
+          v[q] = cur.src;
+        } else {
+          const int64_t rb = (int64_t)cur.src * 8 + (int64_t)(i - run_start(cur)) * w - g.sb * 8;
+          const int d = (int)(rb >> 5);
+          const uint32_t lo32 = sh.stage[d], hi32 = sh.stage[d + 1];
+          v[q] = __builtin_amdgcn_alignbit(hi32, lo32, (uint32_t)rb & 31) & mask;
+        }
+      }
+    }
+    sink.put(i0, v, cnt);
+  }
+}
+
+// Sink: void put(uint32_t i0, const uint32_t (&v)[8], int cnt)  (cnt <= 8 values from i0)
+template <class Sink>
+__device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __restrict__ runs_, const BlockDesc* __restrict__ blks_,
                               int64_t count, ExpandShared& sh, Sink& sink) {
   const int lane = lane_id();
   const int w = S.w;
   const uint32_t mask = w == 32 ? 0xffffffffu : ((1u << w) - 1);
   if (count > S.produced) count = S.produced;
-  const int64_t nblk = (count + kHBlock - 1) / kHBlock;
-  const RunEnt* R = runs + S.run_base;
-  for (int64_t k = 0; k < nblk; k++) {
-    const int64_t v0 = k * kHBlock;
-    const int64_t v1 = v0 + kHBlock < count ? v0 + kHBlock : count;
-    const int r0 = blks[S.blk_base + k];
-    const int r1 = (k + 1 < nblk) ? blks[S.blk_base + k + 1] : S.n_runs - 1;
-    const int nr = r1 - r0 + 1;  // <= kHBlock + 1
-    // runs [r0, r1] plus the entry after r1 (its start ends run r1)
-    for (int i = lane; i <= nr; i += 64) {
-      RunEnt e;
-      if (r0 + i < S.n_runs) e = R[r0 + i];
-      else { e.start = (uint32_t)S.produced; e.src = 0; }
-      sh.runs[i] = e;
+  if (count <= 0) return;
+  const uint32_t end_all = (uint32_t)count;
+  const gcu8 sp = gconst(S.p);
+  const int64_t n = S.n;
+  const PQG_G RunEnt* runs = gconst(runs_) + S.run_base;
+  const PQG_G BlockDesc* blks = gconst(blks_) + S.blk_base;
+  const int nb_all = S.n_blocks;
+  for (int b0 = 0; b0 < nb_all; b0 += 64) {
+    const int nb = nb_all - b0 < 64 ? nb_all - b0 : 64;
+    __builtin_amdgcn_wave_barrier();
+    if (lane < nb) {
+      const PQG_G BlockDesc& d = blks[b0 + lane];
+      sh.desc[lane].v0 = d.v0;
+      sh.desc[lane].r0 = d.r0;
+      sh.desc[lane].lo = d.lo;
+      sh.desc[lane].nbytes = d.nbytes;
+      sh.desc[lane].nr = d.nr;
     }
     __builtin_amdgcn_wave_barrier();
-    // payload bytes of the block's bit-packed values
-    int64_t lo = INT64_MAX, hi = -1;
-    for (int i = lane; i < nr; i += 64) {
-      const RunEnt e = sh.runs[i];
-      if (!(e.start & kRunBP)) continue;
-      const int64_t s0 = run_start(e), s1 = run_start(sh.runs[i + 1]);
-      const int64_t f = s0 > v0 ? s0 : v0, l = s1 < v1 ? s1 : v1;
-      if (f >= l) continue;
-      const int64_t b0 = (int64_t)e.src * 8 + (f - s0) * w, b1 = (int64_t)e.src * 8 + (l - s0) * w;
-      lo = b0 >> 3 < lo ? b0 >> 3 : lo;
-      hi = (b1 + 7) >> 3 > hi ? (b1 + 7) >> 3 : hi;
+    int nk = nb;  // blocks starting at or past `count` are not needed
+    while (nk > 0 && sh.desc[nk - 1].v0 >= end_all) nk--;
+    if (nk == 0) break;
+    // values of the last block here end at the next batch's first block, or at count
+    uint32_t tail_end = end_all;
+    if (nk == nb && b0 + nb < nb_all) {
+      const uint32_t nv0 = blks[b0 + nb].v0;
+      tail_end = nv0 < end_all ? nv0 : end_all;
     }
-    lo = wave_min(lo);
-    hi = -wave_min(-hi);
-    // staged from the 4-aligned address at or below byte lo: stream byte sb
-    // (sb may be up to 3 bytes before the stream; those bytes are never used)
-    const int64_t sb = lo - (int64_t)(((uintptr_t)S.p + (uintptr_t)lo) & 3);
-    const bool staged = hi > lo && hi - sb <= kStageBytes;
-    if (staged) {
-      const int nd = (int)((hi - sb + 3) >> 2) + 1;
-      for (int d = lane; d < nd; d += 64) {
-        const int64_t b = sb + 4 * (int64_t)d;
-        uint32_t x = 0;
-        // a dword holding a byte < n is mapped; bytes at or past n read as 0 (Q5)
-        if (b + 4 <= S.n) x = *(const uint32_t*)(S.p + b);
-        else if (b < S.n) x = *(const uint32_t*)(S.p + b) & (0xffffffffu >> (8 * (4 - (S.n - b))));
-        sh.stage[d] = x;
+    BlockRegs A, B;
+    BlockGeom ga = block_geom(sh, 0, nk, tail_end, S), gb;
+    block_fetch(A, ga, runs, sp, n, lane);
+    for (int k = 0; k < nk; k += 2) {
+      if (k + 1 < nk) {
+        gb = block_geom(sh, k + 1, nk, tail_end, S);
+        block_fetch(B, gb, runs, sp, n, lane);
       }
+      block_process(A, ga, sh, S, mask, w, lane, sink);
+      if (k + 1 >= nk) break;
+      if (k + 2 < nk) {
+        ga = block_geom(sh, k + 2, nk, tail_end, S);
+        block_fetch(A, ga, runs, sp, n, lane);
+      }
+      block_process(B, gb, sh, S, mask, w, lane, sink);
     }
-    __builtin_amdgcn_wave_barrier();
-    // 8 consecutive values per lane
-    const int64_t i0 = v0 + lane * 8;
-    if (i0 < v1) {
-      const int cnt = (int)(v1 - i0 < 8 ? v1 - i0 : 8);
-      int lo2 = 0, hi2 = nr - 1;  // last run with start <= i0
-      while (lo2 < hi2) {
-        const int mid = (lo2 + hi2 + 1) >> 1;
-        if ((int64_t)run_start(sh.runs[mid]) <= i0) lo2 = mid; else hi2 = mid - 1;
-      }
-      int r = lo2;
-      RunEnt cur = sh.runs[r];
-      int64_t nxt = run_start(sh.runs[r + 1]);
-      uint32_t v[8];
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const int64_t i = i0 + q;
-        v[q] = 0;
-        if (q < cnt) {
-          while (i >= nxt && r + 1 < nr) {
-            r++;
-            cur = sh.runs[r];
-            nxt = run_start(sh.runs[r + 1]);
-          }
-          if (!(cur.start & kRunBP)) {
-            v[q] = cur.src;
-          } else {
-            const int64_t bit = (int64_t)cur.src * 8 + (i - run_start(cur)) * w;
-            if (staged) {
-              const int64_t rb = bit - sb * 8;
-              const int d = (int)(rb >> 5);
-              const uint64_t x = (uint64_t)sh.stage[d] | ((uint64_t)sh.stage[d + 1] << 32);
-              v[q] = (uint32_t)(x >> (rb & 31)) & mask;
-            } else {
-              v[q] = extract_global(S.p, S.n, bit, w);
-            }
-          }
-        }
-      }
-      sink.put(i0, v, cnt);
-    }
-    __builtin_amdgcn_wave_barrier();
   }
+  __builtin_amdgcn_wave_barrier();
 }
 
 }  // namespace pqg

@@ -28,9 +28,9 @@ namespace pqg {
 
 // ---- K3a ---------------------------------------------------------------------
 __device__ __forceinline__ int reg_stream(JobDev& job, HStream* streams, int32_t* slot, int pidx, int kind,
-                                          const uint8_t* p, int64_t n, int w, int64_t count) {
+                                          gcu8 p, int64_t n, int w, int64_t count) {
   const int64_t nruns = n / 2 + 2;  // every run but a truncated last one takes >= 2 bytes
-  const int64_t nblks = count / kHBlock + 2;
+  const int64_t nblks = count / kHBlock + nruns / kHBlockRuns + 2;  // blocks close at kHBlock values or kHBlockRuns runs
   const int64_t rb = (int64_t)atomicAdd((unsigned long long*)&job.run_used, (unsigned long long)nruns);
   const int64_t bb = (int64_t)atomicAdd((unsigned long long*)&job.blk_used, (unsigned long long)nblks);
   if (rb + nruns > job.run_cap || bb + nblks > job.blk_cap) {
@@ -39,7 +39,7 @@ __device__ __forceinline__ int reg_stream(JobDev& job, HStream* streams, int32_t
   }
   const int id = pidx * 3 + (kind > 2 ? 2 : kind);
   HStream& S = streams[id];
-  S.p = p;
+  S.p = (const uint8_t*)p;
   S.n = n;
   S.run_base = job.run_base + rb;
   S.blk_base = job.blk_base + bb;
@@ -50,7 +50,7 @@ __device__ __forceinline__ int reg_stream(JobDev& job, HStream* streams, int32_t
   S.n_runs = 0;
   S.produced = 0;
   S.status = kOK;
-  S.pad = 0;
+  S.n_blocks = 0;
   *slot = id;
   return id;
 }
@@ -66,7 +66,7 @@ __global__ void __launch_bounds__(256) k_page_setup(JobDev* jobs, PageDev* pages
     JobDev& job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
     // ---- the page block and its level / value streams (read phase)
-    const uint8_t* block;
+    gcu8 block;
     int64_t blen;
     int32_t levels = 0;
     if (pg.page_type == 3) {
@@ -76,9 +76,9 @@ __global__ void __launch_bounds__(256) k_page_setup(JobDev* jobs, PageDev* pages
     } else {
       blen = pg.scratch_offset >= 0 ? pg.usize : pg.csize;
     }
-    if (pg.scratch_offset >= 0) block = scratch + job.scratch_base + pg.scratch_offset;
-    else block = job.data + pg.payload_offset + (levels > 0 ? levels : 0);
-    const uint8_t *rep = nullptr, *def = nullptr;
+    if (pg.scratch_offset >= 0) block = gconst(scratch) + job.scratch_base + pg.scratch_offset;
+    else block = gconst(job.data) + pg.payload_offset + (levels > 0 ? levels : 0);
+    gcu8 rep = nullptr, def = nullptr;
     int64_t rep_n = -1, def_n = -1;  // -1: the level decoder is not initialised
     int64_t vpos = 0;
     int e = kOK;
@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(256) k_page_setup(JobDev* jobs, PageDev* pages
       }
     } else {
       // V2: raw level bytes, a decoder only for a non-empty section (page_v2.go:110-120)
-      const uint8_t* lv = job.data + pg.payload_offset;
+      gcu8 lv = gconst(job.data) + pg.payload_offset;
       if (levels > 0 && pg.rep_len > 0) { rep = lv; rep_n = pg.rep_len; }
       if (levels > 0 && pg.def_len > 0) { def = lv + pg.rep_len; def_n = levels - pg.rep_len; }
     }
@@ -114,13 +114,13 @@ __global__ void __launch_bounds__(256) k_page_setup(JobDev* jobs, PageDev* pages
       pg.read_status = e;
       continue;
     }
-    pg.block = block;
+    pg.block = (const uint8_t*)block;
     pg.block_len = blen;
-    pg.val = block + vpos;
+    pg.val = (const uint8_t*)(block + vpos);
     pg.val_n = blen - vpos;
-    pg.rep = rep;
+    pg.rep = (const uint8_t*)rep;
     pg.rep_n = rep_n;
-    pg.def = def;
+    pg.def = (const uint8_t*)def;
     pg.def_n = def_n;
     const int64_t n = pg.num_values;
     if (n > 0) {
@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(256) k_page_setup(JobDev* jobs, PageDev* pages
     }
     // values: RLE_DICTIONARY indices (first byte = bit width) / RLE booleans (u32 length)
     const int64_t vn = blen - vpos;
-    const uint8_t* val = block + vpos;
+    gcu8 val = block + vpos;
     if (pg.encoding == 8 && vn >= 1) {
       const int w = val[0];
       pg.dict_width = w;
@@ -145,104 +145,208 @@ __global__ void __launch_bounds__(256) k_page_setup(JobDev* jobs, PageDev* pages
 }
 
 // ---- K3b ---------------------------------------------------------------------
-// readUVariant32 (helpers.go:149-165) over the lane's byte reader.
-__device__ __forceinline__ int lane_uvar32(LaneBytes& rd, int64_t& pos, uint32_t* out) {
-  uint64_t x = 0;
-  unsigned s = 0;
-  for (int i = 0;; i++) {
-    const int b = rd.get(pos);
-    if (b < 0) return kEOF;
-    pos++;
-    if (b < 0x80) {
-      if (i > 9 || (i == 9 && b > 1)) return kRLE;
-      x |= (s < 64 ? (uint64_t)b << s : 0);
-      if (x > 0x7fffffffull) return kRLE;
-      *out = (uint32_t)x;
-      return kOK;
+// One lane walks one stream.  The lane's window on its stream: 64-byte chunks
+// (16-byte aligned in memory); the chunk holding `pos` and the next one sit in
+// two LDS slots and the one after is prefetched into registers, so the walk
+// waits on global memory about once per 64 bytes, for a load issued a chunk
+// earlier.  Positions are 32-bit (a page is < 2 GiB: its sizes are thrift
+// i32); the per-run path is kept short because a single wave per SIMD walks
+// it with nothing to hide its latency behind.
+constexpr int kWalkThreads = 256;
+
+struct LaneRing {
+  gcu8 base;       // 16-byte aligned address at or below the stream start
+  uint32_t n;      // stream bytes
+  uint32_t d0;     // stream byte 0 is byte d0 of chunk 0
+  uint32_t cur;    // chunk of the current position (slots hold cur, cur+1)
+  PQG_L uint32_t* lds;  // dword k of slot s at lds[(16 s + k) * kWalkThreads]
+
+  // Load chunk c into its slot.  No prefetch is carried in registers across
+  // iterations: a loop-carried register holding an in-flight load makes the
+  // compiler wait for it (vmcnt(0)) at every iteration's latch, and that wait
+  // also covers the run-table store just issued.
+  __device__ __forceinline__ void load(uint32_t c) {
+    uint4 r[4];
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      // granule [c*64 + 16g - d0, +16): mapped when it holds a stream byte < n
+      const int64_t s0 = (int64_t)c * 64 + 16 * g - d0;
+      r[g] = (s0 < (int64_t)n && s0 + 16 > 0) ? ldg16((uintptr_t)(base + (size_t)c * 64 + 16 * g))
+                                               : make_uint4(0, 0, 0, 0);
     }
-    if (s < 64) x |= (uint64_t)(b & 0x7f) << s;
-    s += 7;
+    PQG_L uint32_t* b = lds + (c & 1) * 16 * kWalkThreads;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      b[(4 * g + 0) * kWalkThreads] = r[g].x;
+      b[(4 * g + 1) * kWalkThreads] = r[g].y;
+      b[(4 * g + 2) * kWalkThreads] = r[g].z;
+      b[(4 * g + 3) * kWalkThreads] = r[g].w;
+    }
   }
-}
+  __device__ __forceinline__ void move_to(uint32_t c) {
+    if (c != cur + 1) load(c);  // a jump: both chunks are new
+    load(c + 1);
+    cur = c;
+  }
+  __device__ __forceinline__ void init(const uint8_t* p, uint32_t n_, PQG_L uint32_t* lds_) {
+    d0 = (uint32_t)((uintptr_t)p & 15);
+    base = gconst(p) - d0;
+    n = n_;
+    lds = lds_;
+    cur = 0xfffffff0u;
+    move_to(0);
+  }
+  // 8 bytes at stream position pos (< n; bytes past n are garbage)
+  __device__ __forceinline__ uint64_t peek8(uint32_t pos) {
+    const uint32_t off = pos + d0;
+    const uint32_t c = off >> 6;
+    if (c != cur) move_to(c);
+    const uint32_t k0 = ((c & 1) << 4) | ((off >> 2) & 15);
+    const uint32_t a = lds[k0 * kWalkThreads], b = lds[((k0 + 1) & 31) * kWalkThreads],
+                   cc = lds[((k0 + 2) & 31) * kWalkThreads];
+    const uint32_t sh = (off & 3) * 8;
+    const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sh), hi = __builtin_amdgcn_alignbit(cc, b, sh);
+    return (uint64_t)lo | (uint64_t)hi << 32;
+  }
+};
 
 // Lanes [0, total) walk the rep streams, [total, 2 total) the def streams,
 // [2 total, 3 total) the value streams, so a wave's lanes do alike work.
-__global__ void __launch_bounds__(256) k_hybrid_walk(const PageDev* pages, const int* list, const int* total,
-                                                     HStream* streams, RunEnt* runs, int32_t* blks) {
+__global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pages, const int* list, const int* total,
+                                                              HStream* streams, RunEnt* runs, BlockDesc* blks) {
+  __shared__ uint32_t buf[32 * kWalkThreads];  // two 64-byte chunks per lane
   const int nt = *total;
-  for (int g = blockIdx.x * 256 + threadIdx.x; g < 3 * nt; g += gridDim.x * 256) {
+  for (int g = blockIdx.x * kWalkThreads + threadIdx.x; g < 3 * nt; g += gridDim.x * kWalkThreads) {
     const int kind = g / nt;
     const PageDev& pg = pages[list[g - kind * nt]];
     const int hs = kind == 0 ? pg.hs_rep : kind == 1 ? pg.hs_def : pg.hs_val;
     if (hs < 0) continue;
     HStream& S = streams[hs];
-    const int w = S.w;
-    const int64_t n = S.n, count = S.count;
-    const int rb = (w + 7) / 8;
-    RunEnt* R = runs + S.run_base;
-    int32_t* B = blks + S.blk_base;
-    LaneBytes rd;
-    rd.init(S.p, n);
-    int64_t pos = 0, produced = 0, next_blk = 0;
-    int nr = 0, status = kOK;
+    const uint32_t w = (uint32_t)S.w;
+    const uint32_t n = (uint32_t)S.n, count = (uint32_t)S.count;
+    const uint32_t rb = (w + 7) >> 3;
+    const uint64_t vmask = rb >= 4 ? 0xffffffffull : ((1ull << (8 * rb)) - 1);
+    PQG_G uint32_t* R = (PQG_G uint32_t*)(gmut(runs) + S.run_base);
+    PQG_G uint32_t* B = (PQG_G uint32_t*)(gmut(blks) + S.blk_base);
+    LaneRing rd;
+    rd.init(S.p, n, lds_ptr(buf) + threadIdx.x);
+    uint32_t pos = 0, produced = 0, nr = 0;
+    int status = kOK;
+    // block under construction (see BlockDesc)
+    uint32_t nb = 0, bv0 = 0, br0 = 0, bn = 0;
+    uint64_t blo = ~0ull, bhi = 0;
+    auto close_block = [&]() {
+      if (bn == 0) return;
+      const uint32_t lo = blo == ~0ull ? 0u : (uint32_t)blo;
+      const uint32_t nbytes = blo == ~0ull ? 0u : (uint32_t)(bhi - blo);
+      PQG_G uint32_t* d = B + 4 * nb;
+      stg16((uintptr_t)d, make_uint4(bv0, br0, lo, (nbytes & 0xffff) | (bn << 16)));
+      nb++;
+    };
     while (produced < count) {
-      uint32_t h;
-      int e = lane_uvar32(rd, pos, &h);
-      if (e) { status = e; break; }
-      int64_t take;
-      RunEnt ent;
+      // hybridDecoder.next: run header = readUVariant32 (helpers.go:149-165)
+      if (pos >= n) { status = kEOF; break; }
+      uint64_t x = rd.peek8(pos);
+      uint32_t h, hl;
+      if ((x & 0x80) == 0) {
+        h = (uint32_t)x & 0x7f;
+        hl = 1;
+      } else {  // multi-byte header: exactly binary.ReadUvarint + the MaxInt32 check
+        uint64_t v = 0;
+        unsigned sft = 0;
+        int e = kOK;
+        hl = 0;
+        for (uint32_t i = 0;; i++) {
+          if (pos + i >= n) { e = kEOF; break; }
+          const uint32_t b = i < 8 ? (uint32_t)(x >> (8 * i)) & 0xff : (uint32_t)rd.peek8(pos + i) & 0xff;
+          if (b < 0x80) {
+            if (i > 9 || (i == 9 && b > 1)) e = kRLE;  // overflows uint64
+            else {
+              v |= sft < 64 ? (uint64_t)b << sft : 0;
+              if (v > 0x7fffffffull) e = kRLE;  // > MaxInt32
+            }
+            hl = i + 1;
+            break;
+          }
+          if (sft < 64) v |= (uint64_t)(b & 0x7f) << sft;
+          sft += 7;
+        }
+        if (e) { status = e; break; }
+        h = (uint32_t)v;
+        x = rd.peek8(pos + hl) << 8;  // the RLE value at byte 1, like the fast path
+      }
+      pos += hl;
+      uint32_t take, st, src;
+      const uint32_t left = count - produced;
       if (h & 1) {  // bit-packed: h>>1 groups of 8 values, w bytes each
-        const int64_t groups = h >> 1;
+        const uint32_t groups = h >> 1;
         if (groups == 0) { status = kRLE; break; }  // "empty bit-packed run"
-        take = groups * 8 < count - produced ? groups * 8 : count - produced;
-        const int64_t need = (take + 7) / 8;
-        // groups whose first byte is inside the stream; a short read is zero padded
-        const int64_t ok = pos < n ? (n - pos + w - 1) / w : 0;
-        if (ok < need) {
+        take = groups >= (left + 7) >> 3 ? left : groups * 8;
+        const uint32_t need = (take + 7) >> 3;
+        // every group read must start inside the stream; a short one is zero padded (Q5)
+        if ((uint64_t)pos + (uint64_t)(need - 1) * w >= n) {
+          const uint32_t ok = pos < n ? (n - pos + w - 1) / w : 0;
           take = ok * 8;
           status = kEOF;
         }
-        ent.start = (uint32_t)produced | kRunBP;
-        ent.src = (uint32_t)pos;
-        pos += groups * w;
+        st = produced | kRunBP;
+        src = pos;
+        pos = (uint64_t)pos + (uint64_t)groups * w > 0xffffffffull ? 0xffffffffu : pos + groups * w;
       } else {  // RLE: h>>1 repeats of a ceil(w/8)-byte little-endian value
-        const int64_t cnt = h >> 1;
+        const uint32_t cnt = h >> 1;
         if (cnt == 0) { status = kRLE; break; }
         if (pos >= n || n - pos < rb) { status = kEOF; break; }
-        uint32_t v = 0;
-        for (int k = 0; k < rb; k++) v |= (uint32_t)rd.get(pos + k) << (8 * k);
+        src = (uint32_t)((x >> 8) & vmask);
         pos += rb;
-        if (w < 32 && (v >> w) != 0) { status = kRLE; break; }  // readRLERunValue :127-129
-        take = cnt < count - produced ? cnt : count - produced;
-        ent.start = (uint32_t)produced;
-        ent.src = v;
+        if (w < 32 && (src >> w) != 0) { status = kRLE; break; }  // readRLERunValue :127-129
+        take = cnt < left ? cnt : left;
+        st = produced;
       }
       if (take > 0) {
-        R[nr] = ent;
-        produced += take;
-        while (next_blk * kHBlock < produced) B[next_blk++] = nr;
+        stg8((uintptr_t)(R + 2 * nr), st, src);
+        // the run joins the open block, and every block it reaches into
+        const uint32_t rend = produced + take;
+        for (uint32_t v = produced; v < rend;) {
+          if (bn == kHBlockRuns || v >= bv0 + kHBlock) {
+            close_block();
+            bv0 = v;
+            br0 = nr;
+            bn = 0;
+            blo = ~0ull;
+            bhi = 0;
+          }
+          bn++;
+          const uint32_t pe = rend < bv0 + kHBlock ? rend : bv0 + kHBlock;
+          if (st & kRunBP) {
+            const uint64_t b0 = ((uint64_t)src * 8 + (uint64_t)(v - produced) * w) >> 3;
+            const uint64_t b1 = ((uint64_t)src * 8 + (uint64_t)(pe - produced) * w + 7) >> 3;
+            blo = b0 < blo ? b0 : blo;
+            bhi = b1 > bhi ? b1 : bhi;
+          }
+          v = pe;
+        }
+        produced = rend;
         nr++;
       }
       if (status) break;
     }
-    S.n_runs = nr;
+    close_block();
+    S.n_runs = (int32_t)nr;
     S.produced = (int32_t)produced;
     S.status = status;
+    S.n_blocks = (int32_t)nb;
   }
 }
 
 // ---- K3c ---------------------------------------------------------------------
 struct LevelSink {
-  uint8_t* out;
+  gu8 out;
   uint32_t maxl;
   int64_t nn;
-  __device__ __forceinline__ void put(int64_t i0, const uint32_t (&v)[8], int cnt) {
-    uint8_t* o = out + i0;
+  __device__ __forceinline__ void put(uint32_t i0, const uint32_t (&v)[8], int cnt) {
+    gu8 o = out + i0;
     if (cnt == 8 && ((uintptr_t)o & 7) == 0) {
-      uint2 x;
-      x.x = v[0] | v[1] << 8 | v[2] << 16 | v[3] << 24;
-      x.y = v[4] | v[5] << 8 | v[6] << 16 | v[7] << 24;
-      *(uint2*)o = x;
+      stg8((uintptr_t)o, v[0] | v[1] << 8 | v[2] << 16 | v[3] << 24, v[4] | v[5] << 8 | v[6] << 16 | v[7] << 24);
     } else {
       for (int q = 0; q < cnt; q++) o[q] = (uint8_t)v[q];
     }
@@ -252,18 +356,20 @@ struct LevelSink {
 
 __global__ void __launch_bounds__(64) k_levels_expand(JobDev* jobs, PageDev* pages, const int* list,
                                                       const int* total, int* queue, const HStream* streams,
-                                                      const RunEnt* runs, const int32_t* blks, uint8_t* def_arena,
+                                                      const RunEnt* runs, const BlockDesc* blks, uint8_t* def_arena,
                                                       uint8_t* rep_arena) {
   __shared__ __attribute__((aligned(16))) ExpandShared sh;
   const int lane = lane_id();
   for (;;) {
-    int t = 0;
-    if (lane == 0) t = atomicAdd(queue, 1);
-    t = __shfl(t, 0, 64);
+    const int t = queue_next(queue);
     if (t >= *total) return;
-    PageDev& pg = pages[list[t]];
+    // wave-uniform index: the page / job / stream records below are read once
+    // with scalar loads into locals; read through references, every output
+    // store (which might alias them) would force a re-load and a vmcnt wait
+    const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
+    const PageDev pg = pages[pidx];
     if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3)) continue;
-    const JobDev& job = jobs[pg.job];
+    const JobDev job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
     // readValues (page_v1.go:27-55): rep levels, then def levels, then values
     const int64_t n = pg.num_values;
@@ -274,10 +380,10 @@ __global__ void __launch_bounds__(64) k_levels_expand(JobDev* jobs, PageDev* pag
         if (pg.rep_n < 0) {
           de = kLEVELS;  // V2 with no rep-level bytes: "reader is not initialized"
         } else {
-          const HStream& S = streams[pg.hs_rep];
+          const HStream S = streams[pg.hs_rep];
           if (S.status != kOK) de = S.status;
           else {
-            LevelSink sk{rep_arena + job.slot_base + pg.slot_offset, (uint32_t)job.max_rep, 0};
+            LevelSink sk{gmut(rep_arena) + job.slot_base + pg.slot_offset, (uint32_t)job.max_rep, 0};
             hybrid_expand(S, runs, blks, n, sh, sk);
           }
         }
@@ -287,10 +393,10 @@ __global__ void __launch_bounds__(64) k_levels_expand(JobDev* jobs, PageDev* pag
           if (pg.def_n < 0) {
             de = kLEVELS;
           } else {
-            const HStream& S = streams[pg.hs_def];
+            const HStream S = streams[pg.hs_def];
             if (S.status != kOK) de = S.status;
             else {
-              LevelSink sk{def_arena + job.slot_base + pg.slot_offset, (uint32_t)job.max_def, 0};
+              LevelSink sk{gmut(def_arena) + job.slot_base + pg.slot_offset, (uint32_t)job.max_def, 0};
               hybrid_expand(S, runs, blks, n, sh, sk);
               nn = wave_sum(sk.nn);
             }
@@ -301,8 +407,8 @@ __global__ void __launch_bounds__(64) k_levels_expand(JobDev* jobs, PageDev* pag
       }
     }
     if (lane == 0) {
-      pg.not_null = (int32_t)nn;
-      if (de != kOK) pg.decode_status = de;
+      pages[pidx].not_null = (int32_t)nn;
+      if (de != kOK) pages[pidx].decode_status = de;
     }
   }
 }

@@ -18,8 +18,9 @@
 #include "pqg_common.h"
 
 namespace pqg {
-__global__ void k_page_cands(JobDev* jobs, int n_jobs, int* tile_count, int* tile_okc, int64_t* cand_pos);
-__global__ void k_cand_parse(JobDev* jobs, int n_jobs, int64_t total_tiles, const int* tile_count, int* tile_okc,
+__global__ void k_page_cands(JobDev* jobs, int n_jobs, int* tile_count, int* tile_okc, int64_t* cand_pos,
+                             int* cand_list, int* cand_total);
+__global__ void k_cand_parse(JobDev* jobs, int n_jobs, const int* cand_list, const int* cand_total, int* tile_okc,
                              const int64_t* cand_pos, Cand* cands);
 __global__ void k_tile_scan(JobDev* jobs, const int* tile_count, const int* tile_okc, int* tile_off, int* tile_okoff);
 __global__ void k_cand_link(JobDev* jobs, int n_jobs, int64_t total_tiles, const int* tile_count,
@@ -34,13 +35,13 @@ __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const in
 __global__ void k_page_setup(JobDev* jobs, PageDev* pages, const int* list, const int* total, uint8_t* scratch,
                              HStream* streams);
 __global__ void k_hybrid_walk(const PageDev* pages, const int* list, const int* total, HStream* streams,
-                              RunEnt* runs, int32_t* blks);
+                              RunEnt* runs, BlockDesc* blks);
 __global__ void k_levels_expand(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
-                                const HStream* streams, const RunEnt* runs, const int32_t* blks, uint8_t* def_arena,
+                                const HStream* streams, const RunEnt* runs, const BlockDesc* blks, uint8_t* def_arena,
                                 uint8_t* rep_arena);
 __global__ void k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch);
 __global__ void k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
-                         uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const int32_t* blks);
+                         uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks);
 __global__ void k_finalize(JobDev* jobs, int n_jobs, PageDev* pages);
 }  // namespace pqg
 
@@ -97,6 +98,7 @@ struct pqg_ctx {
   DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
   DevBuf tile_count, tile_okc, tile_off, tile_okoff, cand_pos, cands, succ, idx2slot, ok2slot, order;  // K1
   DevBuf streams, runs, blks;  // K3 hybrid run tables
+  DevBuf cand_list;
   int64_t total_tiles = 0;
   JobDev* h_jobs = nullptr;  // pinned
   int h_jobs_cap = 0;
@@ -163,7 +165,7 @@ void pqg_ctx_destroy(pqg_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (auto& e : c->ev) hipEventDestroy(e);
   for (DevBuf* b : {&c->jobs, &c->pages, &c->list, &c->counters, &c->def_arena, &c->rep_arena, &c->value_arena,
-                    &c->scratch, &c->streams, &c->runs, &c->blks, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
+                    &c->scratch, &c->streams, &c->runs, &c->blks, &c->cand_list, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
                     &c->ok2slot, &c->order})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
@@ -255,7 +257,7 @@ static int plan_batch(pqg_ctx* c) {
     d.run_cap = rcap;
     d.run_base = run_total;
     run_total += rcap;
-    int64_t bcap = 3 * (scap / kHBlock + 2 * pcap) + 64;
+    int64_t bcap = 3 * (scap / kHBlock + 2 * pcap) + rcap / kHBlockRuns + 64;
     if (c->force_blks[(size_t)i] > 0) bcap = c->force_blks[(size_t)i];
     d.blk_cap = bcap;
     d.blk_base = blk_total;
@@ -275,12 +277,13 @@ static int plan_batch(pqg_ctx* c) {
       c->tile_okoff.grow(sizeof(int) * (size_t)tile_total + 64) ||
       c->ok2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->cand_pos.grow(sizeof(int64_t) * (size_t)tile_total * kCandPerTile + 64) ||
+      c->cand_list.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->cands.grow(sizeof(Cand) * (size_t)tile_total * kCandPerTile + 64) ||
       c->succ.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->idx2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->order.grow(sizeof(int) * (size_t)page_total + 64) ||
       c->streams.grow(sizeof(HStream) * 3 * (size_t)page_total + 64) || c->runs.grow(sizeof(RunEnt) * (size_t)run_total + 64) ||
-      c->blks.grow(sizeof(int32_t) * (size_t)blk_total + 64))
+      c->blks.grow(sizeof(BlockDesc) * (size_t)blk_total + 64))
     return PQG_ERR_HIP;
   c->total_tiles = tile_total;
   return hip_ok(hipMemcpyAsync(c->jobs.p, c->h_jobs, sizeof(JobDev) * (size_t)n, hipMemcpyHostToDevice, c->stream));
@@ -307,9 +310,12 @@ static int launch_pipeline(pqg_ctx* c) {
   int* tokoff = (int*)c->tile_okoff.p;
   if (nt > 0) {
     int64_t* cpos = (int64_t*)c->cand_pos.p;
-    hipLaunchKernelGGL(k_page_cands, dim3((unsigned)nt), dim3(256), 0, s, jobs, n, tcount, tokc, cpos);
-    hipLaunchKernelGGL(k_cand_parse, dim3((unsigned)((nt * kCandPerTile + 255) / 256)), dim3(256), 0, s, jobs, n, nt,
-                       tcount, tokc, cpos, cands);
+    int* clist = (int*)c->cand_list.p;
+    int* ctotal = ctr + 16;  // zeroed below, counted by k_page_cands
+    hipMemsetAsync(ctotal, 0, sizeof(int), s);
+    hipLaunchKernelGGL(k_page_cands, dim3((unsigned)nt), dim3(256), 0, s, jobs, n, tcount, tokc, cpos, clist, ctotal);
+    hipLaunchKernelGGL(k_cand_parse, dim3((unsigned)std::min<int64_t>((nt * kCandPerTile + 255) / 256, c->num_cus * 4)),
+                       dim3(256), 0, s, jobs, n, clist, ctotal, tokc, cpos, cands);
   }
   hipLaunchKernelGGL(k_tile_scan, dim3(n), dim3(1024), 0, s, jobs, tcount, tokc, toff, tokoff);
   if (nt > 0)
@@ -329,7 +335,7 @@ static int launch_pipeline(pqg_ctx* c) {
   if (c->timed) hipEventRecord(c->ev[3], s);
   HStream* streams = (HStream*)c->streams.p;
   RunEnt* runs = (RunEnt*)c->runs.p;
-  int32_t* blks = (int32_t*)c->blks.p;
+  BlockDesc* blks = (BlockDesc*)c->blks.p;
   const unsigned lane_blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((c->list_cap + 255) / 256, c->num_cus * 4));
   hipLaunchKernelGGL(k_page_setup, dim3(lane_blocks), dim3(256), 0, s, jobs, pages, list, ctr, scratch, streams);
   if (c->timed) hipEventRecord(c->ev[4], s);

@@ -11,7 +11,7 @@ namespace pqg {
 // Byte source over the LDS window, for the thrift reader of the serial walk.
 struct WinSrc {
   Window w;  // by value: the parser state stays in registers
-  __device__ int get(int64_t i) { return w.get(i); }
+  __device__ __forceinline__ int get(int64_t i) { return w.get(i); }
 };
 
 
@@ -47,7 +47,7 @@ struct WinSrc {
 // an earlier page of the walk was a dictionary page.  Sets *next to the
 // position of the following page and *comp to the scratch bytes (16-rounded)
 // the page's decompressed block needs.
-__device__ int classify_page(const JobDev& job, const PageHdr& h, int e, int64_t payload, bool dict_seen,
+__device__ __forceinline__ int classify_page(const JobDev& job, const PageHdr& h, int e, int64_t payload, bool dict_seen,
                              PageDev& pg, int64_t* next, int64_t* comp) {
   *comp = 0;
   *next = payload;
@@ -157,12 +157,12 @@ __device__ __forceinline__ void init_job_results(JobDev& job) {
 // chunk (e.g. a thrift list header claiming 2^31 elements).
 constexpr int64_t kCandParseBytes = 1024;
 struct GlobalSrc {
-  const uint8_t* p;
+  gcu8 p;
   int64_t n, limit;
   bool hit;
   uintptr_t gaddr;  // 16-byte granule held in `g` (0: none)
   uint4 g;
-  __device__ int get(int64_t i) {
+  __device__ __forceinline__ int get(int64_t i) {
     if (i >= limit && i < n) {
       hit = true;
       return -1;
@@ -171,7 +171,7 @@ struct GlobalSrc {
     const uintptr_t a = (uintptr_t)(p + i);
     const uintptr_t ga = a & ~(uintptr_t)15;
     if (ga != gaddr) {  // the granule holds byte i < n: mapped
-      g = *(const uint4*)ga;
+      g = ldg16(ga);
       gaddr = ga;
     }
     const int w = (int)((a >> 2) & 3);
@@ -189,10 +189,10 @@ constexpr int kCandFrames = 4, kCandLast = 8;
 
 // One lane parses and classifies the candidate at position p (kept out of
 // line: the scan loop around it must stay small).
-__device__ __noinline__ void parse_candidate(const JobDev& job, int64_t p, SkipFrame* frames, int16_t* lasts,
+__device__ __forceinline__ void parse_candidate(const JobDev& job, int64_t p, SkipFrame* frames, int16_t* lasts,
                                              Cand* out) {
   Compact<GlobalSrc> c;
-  c.src = GlobalSrc{job.data, job.data_len, p + kCandParseBytes, false, 0, make_uint4(0, 0, 0, 0)};
+  c.src = GlobalSrc{gconst(job.data), job.data_len, p + kCandParseBytes, false, 0, make_uint4(0, 0, 0, 0)};
   // Structural pre-check: every thrift writer of PageHeader emits fields 1, 2,
   // 3 in id order with short-form i32 headers (15 t 15 <varint> 15).  A
   // candidate without that shape is not parsed: it is marked kCOMPLEX, which
@@ -247,7 +247,7 @@ __device__ __noinline__ void parse_candidate(const JobDev& job, int64_t p, SkipF
 }
 
 __global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, int n_jobs, int* tile_count, int* tile_okc,
-                                                    int64_t* cand_pos) {
+                                                    int64_t* cand_pos, int* cand_list, int* cand_total) {
   __shared__ int cnt;
   __shared__ int job_s;
   __shared__ int64_t loc[kCandPerTile];
@@ -267,7 +267,7 @@ __global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, int n_jobs, in
   const int64_t lim = job.tcs < job.data_len ? job.tcs : job.data_len;
   const int64_t t0 = (tile - job.tile_base) * kScanTile;
   const int64_t t1 = t0 + kScanTile < lim ? t0 + kScanTile : lim;
-  const uint8_t* base = job.data;
+  const gcu8 base = gconst(job.data);
   const int64_t data_len = job.data_len;
   const uintptr_t a0 = (uintptr_t)(base + t0) & ~(uintptr_t)15;
   for (int64_t off = (int64_t)tid * 16;; off += 256 * 16) {
@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, int n_jobs, in
     const int64_t p0 = (int64_t)(a - (uintptr_t)base);
     if (p0 >= t1) break;
     // the 16-byte granule holds a position < t1 <= data_len, so it is mapped
-    const uint4 v = *(const uint4*)a;
+    const uint4 v = ldg16(a);
     if (!(has_byte_15(v.x) || has_byte_15(v.y) || has_byte_15(v.z) || has_byte_15(v.w))) continue;
     // bytes 16, 17 (lookahead of the last two positions), read only when
     // byte 14 or 15 is 0x15; 0xff (no match) past the end of the buffer
@@ -309,36 +309,39 @@ __global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, int n_jobs, in
     tile_count[tile] = n > kCandPerTile ? kCandPerTile + 1 : n;
     tile_okc[tile] = 0;  // counted by k_cand_parse
   }
+  __shared__ int list_base;
+  if (tid == 0 && n > 0 && n <= kCandPerTile) list_base = atomicAdd(cand_total, n);
+  __syncthreads();
   if (n <= kCandPerTile && tid < n) {  // rank sort by position (positions are distinct)
     const int64_t me = loc[tid];
     int rank = 0;
     for (int k = 0; k < n; k++) rank += loc[k] < me;
     cand_pos[tile * kCandPerTile + rank] = me;
+    cand_list[list_base + tid] = (int)(tile * kCandPerTile + rank);  // slot to parse
   }
 }
 
 // ---- K1a' ------------------------------------------------------------------
 // One lane per candidate slot: parse + classify (kept apart from the byte scan
 // so that the scan has no scratch and runs at full occupancy).
-__global__ void __launch_bounds__(256) k_cand_parse(JobDev* jobs, int n_jobs, int64_t total_tiles,
-                                                    const int* tile_count, int* tile_okc, const int64_t* cand_pos,
+__global__ void __launch_bounds__(256) k_cand_parse(JobDev* jobs, int n_jobs, const int* cand_list,
+                                                    const int* cand_total, int* tile_okc, const int64_t* cand_pos,
                                                     Cand* cands) {
   __shared__ SkipFrame frames[256][kCandFrames];
   __shared__ int16_t lasts[256][kCandLast];
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t tile = g / kCandPerTile;
-  const int s = (int)(g % kCandPerTile);
-  if (tile >= total_tiles) return;
-  const int cntv = tile_count[tile];
-  if (s >= cntv || cntv > kCandPerTile) return;
-  int lo = 0, hi = n_jobs - 1;
-  while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (jobs[mid].tile_base <= tile) lo = mid; else hi = mid - 1;
+  const int nc = *cand_total;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < nc; i += gridDim.x * 256) {
+    const int slot = cand_list[i];
+    const int64_t tile = slot / kCandPerTile;
+    int lo = 0, hi = n_jobs - 1;
+    while (lo < hi) {
+      int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].tile_base <= tile) lo = mid; else hi = mid - 1;
+    }
+    Cand* out = &cands[slot];
+    parse_candidate(jobs[lo], cand_pos[slot], frames[threadIdx.x], lasts[threadIdx.x], out);
+    if (out->status == kOK) atomicAdd(&tile_okc[tile], 1);
   }
-  Cand* out = &cands[tile * kCandPerTile + s];
-  parse_candidate(jobs[lo], cand_pos[tile * kCandPerTile + s], frames[threadIdx.x], lasts[threadIdx.x], out);
-  if (out->status == kOK) atomicAdd(&tile_okc[tile], 1);
 }
 
 // ---- K1b ------------------------------------------------------------------
@@ -628,7 +631,7 @@ __global__ void __launch_bounds__(64) k_scan_pages(JobDev* jobs, PageDev* pages,
   if (j >= n_jobs) return;
   JobDev& job = jobs[j];
   if (!job.scan_fallback) return;
-  Window win{job.data, job.data_len, kFarAway, sh.win};
+  Window win{gconst(job.data), job.data_len, kFarAway, lds_ptr(sh.win)};
   int64_t pos = 0;
   int np = 0;
   int status = kOK;

@@ -22,12 +22,12 @@ struct SnapShared {
   uint8_t out[kSnapLds];
 };
 
-__device__ __forceinline__ uint32_t l2_load_u32(const uint32_t* p) {
+__device__ __forceinline__ uint32_t l2_load_u32(const PQG_G uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool kLds>
-__device__ int snappy_body(Window& win, int64_t s, int64_t slen, uint8_t* dst_g, uint8_t* dst_l, int64_t dlen) {
+__device__ int snappy_body(Window& win, int64_t s, int64_t slen, gu8 dst_g, PQG_L uint8_t* dst_l, int64_t dlen) {
   const int lane = lane_id();
   int64_t d = 0;
   while (s < slen) {
@@ -47,7 +47,7 @@ __device__ int snappy_body(Window& win, int64_t s, int64_t slen, uint8_t* dst_g,
       length = (int64_t)x + 1;
       if (length > dlen - d || length > slen - s) return kSNAPPY;
       // literal copy: source bytes from the compressed block (window source)
-      const uint8_t* src = win.p + s;
+      const gcu8 src = win.p + s;
       for (int64_t i = lane; i < length; i += 64) {
         uint8_t b = src[i];
         if (kLds) dst_l[d + i] = b; else dst_g[d + i] = b;
@@ -84,7 +84,7 @@ __device__ int snappy_body(Window& win, int64_t s, int64_t slen, uint8_t* dst_g,
         b = dst_l[from];
       } else {
         uintptr_t a = (uintptr_t)(dst_g + from);
-        uint32_t wv = l2_load_u32((const uint32_t*)(a & ~(uintptr_t)3));
+        uint32_t wv = l2_load_u32((const PQG_G uint32_t*)(a & ~(uintptr_t)3));
         b = (uint8_t)(wv >> ((a & 3) * 8));
       }
       if (kLds) dst_l[d + i] = b; else dst_g[d + i] = b;
@@ -102,13 +102,12 @@ __global__ void __launch_bounds__(64) k_snappy(JobDev* jobs, PageDev* pages, con
   __shared__ __attribute__((aligned(16))) SnapShared sh;
   const int lane = lane_id();
   for (;;) {
-    int t = 0;
-    if (lane == 0) t = atomicAdd(queue, 1);
-    t = __shfl(t, 0, 64);
+    const int t = queue_next(queue);
     if (t >= *total) return;
-    PageDev& pg = pages[list[t]];
+    const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
+    const PageDev pg = pages[pidx];  // locals via scalar loads (see k_levels_expand)
     if (pg.read_status != kOK || pg.scratch_offset < 0) continue;
-    JobDev& job = jobs[pg.job];
+    const JobDev job = jobs[pg.job];
     // compressed block location (V2: after the raw level bytes)
     int64_t src_off = pg.payload_offset;
     int64_t clen = pg.csize, ulen = pg.usize;
@@ -118,7 +117,7 @@ __global__ void __launch_bounds__(64) k_snappy(JobDev* jobs, PageDev* pages, con
       clen = (int32_t)((uint32_t)pg.csize - (uint32_t)levels);
       ulen = (int32_t)((uint32_t)pg.usize - (uint32_t)levels);
     }
-    Window win{job.data + src_off, clen, kFarAway, sh.win};
+    Window win{gconst(job.data) + src_off, clen, kFarAway, lds_ptr(sh.win)};
     // decodedLen: binary.Uvarint over the block (decode.go:32-43)
     uint64_t v = 0;
     int hl = 0;
@@ -141,10 +140,10 @@ __global__ void __launch_bounds__(64) k_snappy(JobDev* jobs, PageDev* pages, con
     }
     if (e == kOK && v > 0xffffffffull) e = kSNAPPY;
     if (e == kOK && (int64_t)v != ulen) e = kSIZE;
-    uint8_t* dst = scratch + job.scratch_base + pg.scratch_offset;
+    const gu8 dst = gmut(scratch) + job.scratch_base + pg.scratch_offset;
     if (e == kOK) {
       if (ulen <= kSnapLds) {
-        e = snappy_body<true>(win, hl, clen, nullptr, sh.out, ulen);
+        e = snappy_body<true>(win, hl, clen, nullptr, lds_ptr(sh.out), ulen);
         if (e == kOK)
           for (int64_t i = lane; i < ulen; i += 64) dst[i] = sh.out[i];
       } else {
@@ -153,7 +152,7 @@ __global__ void __launch_bounds__(64) k_snappy(JobDev* jobs, PageDev* pages, con
     }
     // V1: getValuesDecoder runs after the block is decompressed (page_v1.go:91-97)
     if (e == kOK && pg.page_type == 0 && !values_supported(job.type, job.type_length, pg.encoding)) e = kUNSUPPORTED;
-    if (lane == 0 && e != kOK) pg.read_status = e;
+    if (lane == 0 && e != kOK) pages[pidx].read_status = e;
   }
 }
 

@@ -23,13 +23,13 @@ namespace pqg {
 // "dict: invalid index" when key >= len(values).  W bytes per entry.
 template <int W>
 struct DictSink {
-  uint8_t* out;
-  const uint8_t* dict;
+  gu8 out;
+  gcu8 dict;
   int64_t count;
   int64_t bad;      // first index with an invalid key
   int64_t nil_key;  // INT96 partial final entry (-1: none): its value reads as zero bytes (Q8)
   int w;            // entry width when W == 0
-  __device__ __forceinline__ void put(int64_t i0, const uint32_t (&v)[8], int cnt) {
+  __device__ __forceinline__ void put(uint32_t i0, const uint32_t (&v)[8], int cnt) {
     bool ok = true;
     for (int q = 0; q < cnt; q++)
       if ((int64_t)v[q] >= count) {
@@ -37,21 +37,19 @@ struct DictSink {
         bad = i0 + q < bad ? i0 + q : bad;
       }
     if (W == 4 && ok && cnt == 8 && ((uintptr_t)(out + i0 * 4) & 15) == 0) {
-      const uint32_t* d = (const uint32_t*)dict;
-      uint4 a = make_uint4(d[v[0]], d[v[1]], d[v[2]], d[v[3]]);
-      uint4 b = make_uint4(d[v[4]], d[v[5]], d[v[6]], d[v[7]]);
-      uint4* o = (uint4*)(out + i0 * 4);
-      o[0] = a;
-      o[1] = b;
+      const PQG_G uint32_t* d = (const PQG_G uint32_t*)dict;
+      const uint4 a = make_uint4(d[v[0]], d[v[1]], d[v[2]], d[v[3]]);
+      const uint4 b = make_uint4(d[v[4]], d[v[5]], d[v[6]], d[v[7]]);
+      stg16((uintptr_t)(out + i0 * 4), a);
+      stg16((uintptr_t)(out + i0 * 4 + 16), b);
       return;
     }
     if (W == 8 && ok && cnt == 8 && ((uintptr_t)(out + i0 * 8) & 15) == 0) {
-      const uint2* d = (const uint2*)dict;
-      uint4* o = (uint4*)(out + i0 * 8);
+      const PQG_G u32x2_t* d = (const PQG_G u32x2_t*)dict;
 #pragma unroll
       for (int q = 0; q < 8; q += 2) {
-        const uint2 x = d[v[q]], y = d[v[q + 1]];
-        o[q / 2] = make_uint4(x.x, x.y, y.x, y.y);
+        const u32x2_t x = d[v[q]], y = d[v[q + 1]];
+        stg16((uintptr_t)(out + i0 * 8 + q * 8), make_uint4(x.x, x.y, y.x, y.y));
       }
       return;
     }
@@ -61,14 +59,14 @@ struct DictSink {
       if (key >= count) continue;
       const int64_t i = i0 + q;
       if (W == 4) {
-        *(uint32_t*)(out + i * 4) = *(const uint32_t*)(dict + key * 4);
+        *(PQG_G uint32_t*)(out + i * 4) = *(const PQG_G uint32_t*)(dict + key * 4);
       } else if (W == 8) {
-        const uint32_t* s = (const uint32_t*)(dict + key * 8);
-        uint32_t* d = (uint32_t*)(out + i * 8);
+        const PQG_G uint32_t* s = (const PQG_G uint32_t*)(dict + key * 8);
+        PQG_G uint32_t* d = (PQG_G uint32_t*)(out + i * 8);
         d[0] = s[0];
         d[1] = s[1];
       } else {
-        const uint8_t* s = dict + key * ww;
+        gcu8 s = dict + key * ww;
         for (int b = 0; b < ww; b++) out[i * ww + b] = (key == nil_key) ? 0 : s[b];
       }
     }
@@ -77,8 +75,8 @@ struct DictSink {
 
 // booleanRLEDecoder (type_boolean.go:100-120): value == 1
 struct BoolSink {
-  uint8_t* out;
-  __device__ __forceinline__ void put(int64_t i0, const uint32_t (&v)[8], int cnt) {
+  gu8 out;
+  __device__ __forceinline__ void put(uint32_t i0, const uint32_t (&v)[8], int cnt) {
     for (int q = 0; q < cnt; q++) out[i0 + q] = v[q] == 1;
   }
 };
@@ -93,6 +91,8 @@ struct DbpShared {
   uint64_t mind[kBlocks];               // min delta (as unsigned for wrapping adds)
   uint8_t widths[kBlocks][kMaxMb];
   int64_t mb_off[kBlocks][kMaxMb];      // stream offset of each miniblock
+  uint8_t gwidths[256];                 // generic path: miniblock widths of the block
+  uint64_t gvals[8];                    // generic path: current 8-group
 };
 
 __device__ __forceinline__ int read_uvarint64(Window& w, int64_t& pos, uint64_t* out) {
@@ -134,10 +134,10 @@ __device__ __forceinline__ int read_u32var_delta(Window& w, int64_t& pos, int32_
 // Values of a DBP page: emulates deltaBitPackDecoder{32,64}.next for positions
 // [0, nn).  Regular layout (miniblock value count a multiple of 8, <= kMaxMb
 // miniblocks): wave-parallel unpack + wrapping scan; otherwise one lane.
-__device__ int dbp_decode(const uint8_t* s, int64_t n, int64_t readable, bool is64, int64_t nn, uint8_t* out,
+__device__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_t nn, gu8 out,
                           DbpShared& sh, int stage /*0 = header only (read phase), 1 = decode*/) {
   const int lane = lane_id();
-  Window win{s, n, kFarAway, sh.win};
+  Window win{s, n, kFarAway, lds_ptr(sh.win)};
   int64_t pos = 0;
   int32_t bs, mbc, total;
   uint64_t first;
@@ -169,9 +169,10 @@ __device__ int dbp_decode(const uint8_t* s, int64_t n, int64_t readable, bool is
     int64_t rp = pos;
     int32_t cur_mb = mbc;  // force header read at position 0 semantics below
     uint64_t mind = 0, prev = first;
-    uint8_t widths[256];
+    uint8_t* widths = sh.gwidths;  // LDS: wave-uniform values (no scratch)
+    uint64_t* vals = sh.gvals;
     int32_t cw = 0, mbpos = 0;
-    uint64_t vals[8] = {0};
+    for (int k = 0; k < 8; k++) vals[k] = 0;
     // init already read the first miniblock header: emulate it
     {
       if ((e = read_signed(win, rp, is64, &mind))) return e;
@@ -211,8 +212,8 @@ __device__ int dbp_decode(const uint8_t* s, int64_t n, int64_t readable, bool is
         }
       }
       if (lane == 0) {
-        if (is64) *(uint64_t*)(out + p * 8) = prev;
-        else *(uint32_t*)(out + p * 4) = (uint32_t)prev;
+        if (is64) stg8((uintptr_t)(out + p * 8), (uint32_t)prev, (uint32_t)(prev >> 32));
+        else *(PQG_G uint32_t*)(out + p * 4) = (uint32_t)prev;
       }
       prev = prev + vals[p % 8] + mind;
       if (!is64) prev = (uint32_t)prev;
@@ -295,8 +296,8 @@ __device__ int dbp_decode(const uint8_t* s, int64_t n, int64_t readable, bool is
       for (int k = 0; k < 4; k++) {
         int64_t p = t0 + lane * 4 + k;
         if (p < p_end) {
-          if (is64) *(uint64_t*)(out + p * 8) = run;
-          else *(uint32_t*)(out + p * 4) = (uint32_t)run;
+          if (is64) stg8((uintptr_t)(out + p * 8), (uint32_t)run, (uint32_t)(run >> 32));
+          else *(PQG_G uint32_t*)(out + p * 4) = (uint32_t)run;
         }
         run += d[k];
       }
@@ -316,26 +317,27 @@ union ValuesShared {
 
 __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total,
                                                int* queue, uint8_t* value_arena, const HStream* streams,
-                                               const RunEnt* runs, const int32_t* blks) {
+                                               const RunEnt* runs, const BlockDesc* blks) {
   __shared__ __attribute__((aligned(16))) ValuesShared sh;
   const int lane = lane_id();
   for (;;) {
-    int t = 0;
-    if (lane == 0) t = atomicAdd(queue, 1);
-    t = __shfl(t, 0, 64);
+    const int t = queue_next(queue);
     if (t >= *total) return;
-    PageDev& pg = pages[list[t]];
+    // wave-uniform: page and job records are read once, by scalar loads, into
+    // locals (see k_levels_expand); results are written back at the end
+    const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
+    const PageDev pg = pages[pidx];
     if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3)) continue;
-    JobDev& job = jobs[pg.job];
+    const JobDev job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
-    const uint8_t* val = pg.val;
+    const gcu8 val = gconst(pg.val);
     const int64_t vn = pg.val_n;
     // readable bytes from val (for wide loads)
-    int64_t readable = (pg.scratch_offset >= 0) ? vn : job.data_len - (val - job.data);
+    int64_t readable = (pg.scratch_offset >= 0) ? vn : job.data_len - (pg.val - job.data);
     const int enc = pg.encoding;
     const int64_t nn = pg.not_null;
     const int w = job.value_width;
-    uint8_t* out = value_arena + job.value_base + pg.value_offset * (int64_t)w;
+    const gu8 out = gmut(value_arena) + job.value_base + pg.value_offset * (int64_t)w;
     // ---- valuesDecoder.init (read phase)
     int re = kOK;
     int dict_w = 0;
@@ -351,7 +353,7 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
       if (vn < 4) re = kEOF;
     }
     if (re != kOK) {
-      if (lane == 0) pg.read_status = re;
+      if (lane == 0) pages[pidx].read_status = re;
       continue;
     }
     if (pg.decode_status != kOK || nn == 0) continue;
@@ -366,7 +368,7 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
         int64_t full = vn / 12, rem = vn % 12;
         if (nn > full + (rem > 0 ? 1 : 0)) de = kEOF;
         else {
-          if (nn == full + 1 && rem > 0 && lane == 0) pg.flags |= 1;
+          if (nn == full + 1 && rem > 0 && lane == 0) pages[pidx].flags |= 1;
           for (int64_t i = lane; i < nn * 12; i += 64) out[i] = (i < full * 12) ? val[i] : 0;
         }
       } else if (w > 0 && (w & 3) != 0) {  // FLBA of odd length: byte copy
@@ -381,7 +383,7 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
           for (int64_t i = (int64_t)lane * 4; i < nb; i += 256) {
             if (i + 4 <= nb) {
               uint64_t x = load_u64_masked(val, readable, i, vn);
-              *(uint32_t*)(out + i) = (uint32_t)x;
+              *(PQG_G uint32_t*)(out + i) = (uint32_t)x;
             } else {
               for (int64_t b = i; b < nb; b++) out[b] = val[b];
             }
@@ -391,7 +393,7 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
         de = kUNSUPPORTED;  // PLAIN byte arrays: not in this build yet
       }
     } else if (enc == 8) {
-      const uint8_t* dict = job.dict_data;
+      const gcu8 dict = gconst(job.dict_data);
       const int64_t dcount = job.dict_data ? job.dict_count : 0;
       const int64_t nil_key = (job.flags & 1) ? dcount - 1 : -1;
       if (w == 0) {
@@ -402,7 +404,7 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
         else
           for (int64_t b = lane; b < nn * w; b += 64) out[b] = (0 == nil_key) ? 0 : dict[b % w];
       } else {
-        const HStream& S = streams[pg.hs_val];
+        const HStream S = streams[pg.hs_val];
         const int serr = (S.status != kOK && S.produced < nn) ? S.status : kOK;
         int64_t bad = nn;
         if (w == 4) {
@@ -424,14 +426,14 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
     } else if (enc == 5) {
       de = dbp_decode(val, vn, readable, job.type == 2, nn, out, sh.dbp, 1);
     } else if (enc == 3 && job.type == 0) {  // booleanRLEDecoder: hybrid w=1 after a u32 length
-      const HStream& S = streams[pg.hs_val];
+      const HStream S = streams[pg.hs_val];
       BoolSink sk{out};
       hybrid_expand(S, runs, blks, nn, sh.ex, sk);
       de = (S.status != kOK && S.produced < nn) ? S.status : kOK;
     } else {
       de = kUNSUPPORTED;
     }
-    if (lane == 0 && de != kOK) pg.decode_status = de;
+    if (lane == 0 && de != kOK) pages[pidx].decode_status = de;
   }
 }
 

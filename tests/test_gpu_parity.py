@@ -182,6 +182,15 @@ def _hand_cases():
     cases.append(("levels_empty_rle", U.v1_page(i32([1]), 1, 0, defs=b"\x00\x01"), dict(ptype=abi.INT32, max_def=1)))
     cases.append(("levels_big_rle", U.v1_page(i32([1]), 1, 0, defs=b"\x02\x02"), dict(ptype=abi.INT32, max_def=1)))
     cases.append(("levels_short", U.v1_page(i32([1, 2]), 5, 0, defs=b"\x04\x01"), dict(ptype=abi.INT32, max_def=1)))
+    # run headers as long varints (binary.ReadUvarint accepts zero high bytes up to 10 bytes)
+    one = dict(ptype=abi.INT32, max_def=1)
+    cases.append(("levels_varint6", U.v1_page(i32([1]), 1, 0, defs=b"\x82\x80\x80\x80\x80\x00\x01"), one))
+    cases.append(("levels_varint10", U.v1_page(i32([1]), 1, 0, defs=b"\x82" + b"\x80" * 8 + b"\x00\x01"), one))
+    cases.append(("levels_varint11", U.v1_page(i32([1]), 1, 0, defs=b"\x82" + b"\x80" * 9 + b"\x00\x01"), one))
+    cases.append(("levels_varint_gt_int32", U.v1_page(i32([1]), 1, 0, defs=b"\x80\x80\x80\x80\x10\x01"), one))
+    cases.append(("levels_varint_eof", U.v1_page(i32([1]), 1, 0, defs=b"\x80"), one))
+    cases.append(("levels_bp_2byte_header",
+                  U.v1_page(i32(list(range(800))), 800, 0, defs=b"\xc9\x01" + b"\xff" * 100), one))
     # Q5: short bit-packed group zero padded
     cases.append(("levels_q5", U.v1_page(i32([7]), 3, 0, defs=b"\x03\x01"), dict(ptype=abi.INT32, max_def=1)))
     # V1 level length prefix missing
@@ -365,3 +374,16 @@ def test_scan_garbage_lists_bounded(dec):
     v[1::2] = 0x0101010101010101
     data = W.write_file([W.Column("x", W.INT64, v, rows_per_page=50_000)], n)
     P.compare_file(data, dec)
+
+
+@pytest.mark.parametrize("w", [9, 11, 16, 17, 21, 24, 25, 31, 32])
+def test_dict_index_widths(dec, w):
+    # index streams wider than log2(dictionary size) are valid; mixed RLE / bit-packed runs
+    rng = np.random.default_rng(w)
+    d = 1000
+    dvals = rng.integers(-2**31, 2**31 - 1, size=d).astype(np.int32)
+    dpage = U.page_header_dict(4 * d, 4 * d, d) + dvals.tobytes()
+    for min_rle in (3, 8, 1 << 30):
+        keys = np.repeat(rng.integers(0, d, size=700), rng.integers(1, 12, size=700))[:3000].astype(np.uint32)
+        idx = bytes([w]) + W.hybrid_encode(keys, w, min_rle=min_rle)
+        P.compare_chunk_bytes(dpage + U.v1_page(idx, len(keys), 8), dec, ptype=abi.INT32)
