@@ -218,6 +218,11 @@ int pqg_bench_decode(pqg_ctx* ctx, const pqg_chunk_job* jobs, int n_jobs, int it
  * pages, out[3] = decompressed scratch bytes.  Returns entries written. */
 int pqg_debug_job(pqg_ctx* ctx, int job, int64_t* out, int cap);
 
+/* Diagnostic builds only (compiled with -DPQG_PROFILE): in-kernel phase cycle
+ * counters accumulated since the last call, then reset.  Returns the number of
+ * counters written (0 in normal builds). */
+int pqg_debug_counters(pqg_ctx* ctx, uint64_t* out, int cap);
+
 /* ---- host-side planner: footer / schema (file_meta.go:14-62, schema.go) --- */
 typedef struct pqg_file pqg_file;
 

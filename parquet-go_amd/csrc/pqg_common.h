@@ -110,6 +110,7 @@ struct RunEnt {
 constexpr uint32_t kRunBP = 0x80000000u;
 constexpr int kHBlock = 512;      // values per expander block
 constexpr int kHBlockRuns = 64;   // runs per expander block (one per lane)
+constexpr int kHBlockBytes = 1008;  // payload bytes per block: 64 16-byte granules, aligned anywhere
 
 struct JobDev {
   // ---- inputs

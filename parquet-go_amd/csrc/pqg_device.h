@@ -147,6 +147,18 @@ __device__ __forceinline__ uint64_t extract_bits64(P p, int64_t n, int64_t valid
   return w == 64 ? v : (v & ((1ull << w) - 1));
 }
 
+// In-kernel phase timing (diagnostic builds only: -DPQG_PROFILE).  Lane 0
+// adds s_memtime deltas into pqg_prof[slot]; pqg_debug_counters reads them.
+#ifdef PQG_PROFILE
+static __device__ unsigned long long pqg_prof[64];  // one per translation unit (no -fgpu-rdc)
+#define PQG_T(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#define PQG_ACC(slot, a, b) \
+  do { if (lane_id() == 0) atomicAdd(&pqg_prof[slot], (unsigned long long)((b) - (a))); } while (0)
+#else
+#define PQG_T(var)
+#define PQG_ACC(slot, a, b) do { } while (0)
+#endif
+
 // Next item of an atomic work queue, wave-uniform (in an SGPR): struct loads
 // indexed by it become scalar loads, which do not queue behind vector loads
 // and stores (vmcnt) the way vector loads of the same fields would.

@@ -2,17 +2,21 @@
 //
 // k_hybrid_walk (pqg_levels.hip) turns every hybrid stream into a run table
 // (RunEnt) and block descriptors (BlockDesc: <= kHBlock values, <= kHBlockRuns
-// runs, and the byte range of the bit-packed payload those values use).  An
-// expander wave takes a stream one block at a time: the block's runs and
-// payload bytes are staged in LDS, then every lane produces 8 consecutive
-// values and hands them to a sink (level bytes, dictionary gather, booleans).
-//
-// The loads of block k+1 are issued before block k's sink runs.  vmcnt
-// retires loads and stores in issue order, so a load issued after block k's
-// stores would make its wait cover those stores too; issued before them, it
-// overlaps with block k's gathers and stores.  The two register sets
-// alternate in a 2x unrolled loop, so no in-flight register is copied at the
-// loop latch (a copy would force a full vmcnt(0) wait there).
+// runs and <= kHBlockBytes bytes of bit-packed payload).  An expander wave
+// takes a stream kGroup blocks at a time:
+//   1. every lane issues, for each block of the group, the load of one run
+//      entry and one 16-byte payload granule (unconditionally: a guarded load
+//      is merged with the register's old value at the branch join, and that
+//      copy waits for the load on the spot);
+//   2. one wait, then the runs and payload are installed in LDS;
+//   3. every lane decodes 8 consecutive values of each block (binary search
+//      over the block's runs, w-bit fields from the staged payload);
+//   4. the sink issues all its loads for the group (dictionary gathers) before
+//      any store, then stores.
+// So a group of up to kGroup * kHBlock values costs about two memory round
+// trips per wave (loads, gathers), instead of several per block: vmcnt retires
+// loads and stores in issue order, and each dependent load/wait pair is a
+// full round trip.
 //
 // Values are exactly hybridDecoder.next's (hybrid_decoder.go:82-166): RLE runs
 // repeat their value; bit-packed runs are LSB-first w-bit fields
@@ -23,32 +27,27 @@
 
 namespace pqg {
 
-constexpr int kStageGranules = 192;  // 16-byte payload granules per block (3 per lane)
+constexpr int kGroup = 4;  // blocks per expander step
 
 struct ExpandShared {
   BlockDesc desc[64];
-  RunEnt runs[kHBlockRuns];
-  uint32_t stage[kStageGranules * 4 + 4];
+  RunEnt runs[kGroup][kHBlockRuns];
+  uint32_t stage[kGroup][64 * 4 + 4];  // 64 granules (+ the dword past the end)
+  uint8_t rmap[kGroup][kHBlock];       // run starting at each value of the block (else 0)
 };
 
 __device__ __forceinline__ uint32_t run_start(const RunEnt& r) { return r.start & ~kRunBP; }
-
-// One block's loads, held in registers between issue and install.
-struct BlockRegs {
-  uint32_t rs, rv;   // this lane's run entry
-  uint4 g0, g1, g2;  // this lane's payload granules (lane, lane+64, lane+128)
-};
 
 struct BlockGeom {
   uint32_t v0, v1;  // values [v0, v1)
   uint32_t r0, nr;
   int64_t sb;       // stream offset of stage byte 0 (a 16-byte aligned address)
-  int ng;           // granules staged
+  int ng;           // granules staged (<= 64)
 };
 
 // Block k of the batch in sh.desc[0, nb); `end` bounds the last block.
 __device__ __forceinline__ BlockGeom block_geom(const ExpandShared& sh, int k, int nb, uint32_t end,
-                                                const HStream& S) {
+                                                uintptr_t p) {
   BlockGeom g;
   const BlockDesc& d = sh.desc[k];
   g.v0 = d.v0;
@@ -57,30 +56,10 @@ __device__ __forceinline__ BlockGeom block_geom(const ExpandShared& sh, int k, i
   g.r0 = d.r0;
   g.nr = d.nr;
   const int64_t lo = d.lo;
-  g.sb = lo - (int64_t)(((uintptr_t)S.p + (uintptr_t)lo) & 15);
-  g.ng = d.nbytes ? (int)((lo + d.nbytes - g.sb + 15) >> 4) + 1 : 0;  // +1: the dword pair read past the end
-  if (g.ng > kStageGranules) g.ng = kStageGranules;
+  g.sb = lo - (int64_t)((p + (uintptr_t)lo) & 15);
+  g.ng = d.nbytes ? (int)((lo + d.nbytes - g.sb + 15) >> 4) : 0;
+  if (g.ng > 64) g.ng = 64;
   return g;
-}
-
-// The prefetch loads are unconditional: a load guarded by a branch is merged
-// with the register's old value at the join, and that copy waits (vmcnt) for
-// the load at once.  Lanes with nothing to load read a safe mapped address
-// (`safe`) and block_process ignores the value.
-__device__ __forceinline__ uintptr_t stage_addr(gcu8 sp, int64_t n, int64_t at, bool want, uintptr_t safe) {
-  // a granule holding a stream byte < n is mapped
-  return (want && at < n && at + 16 > 0) ? (uintptr_t)(sp + at) : safe;
-}
-
-__device__ __forceinline__ void block_fetch(BlockRegs& R, const BlockGeom& g, const PQG_G RunEnt* runs, gcu8 sp,
-                                            int64_t n, int lane) {
-  const uint32_t ri = (uint32_t)lane < g.nr ? (uint32_t)lane : 0u;  // nr >= 1
-  R.rs = runs[g.r0 + ri].start;
-  R.rv = runs[g.r0 + ri].src;
-  const uintptr_t safe = (uintptr_t)(runs + g.r0) & ~(uintptr_t)15;
-  R.g0 = ldg16(stage_addr(sp, n, g.sb + 16 * lane, lane < g.ng, safe));
-  R.g1 = ldg16(stage_addr(sp, n, g.sb + 16 * (lane + 64), lane + 64 < g.ng, safe));
-  R.g2 = ldg16(stage_addr(sp, n, g.sb + 16 * (lane + 128), lane + 128 < g.ng, safe));
 }
 
 // zero the bytes of a staged granule at or past the stream end (Q5)
@@ -96,59 +75,54 @@ __device__ __forceinline__ uint4 mask_tail(uint4 v, int64_t at, int64_t n) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-template <class Sink>
-__device__ __forceinline__ void block_process(const BlockRegs& R, const BlockGeom& g, ExpandShared& sh,
-                                              const HStream& S, uint32_t mask, int w, int lane, Sink& sink) {
-  __builtin_amdgcn_wave_barrier();
-  if ((uint32_t)lane < g.nr) {
-    sh.runs[lane].start = R.rs;
-    sh.runs[lane].src = R.rv;
-  }
-  PQG_L uint32_t* st = lds_ptr(sh.stage);
-  if (lane < g.ng) sts16(st + 4 * lane, mask_tail(R.g0, g.sb + 16 * lane, S.n));
-  if (lane + 64 < g.ng) sts16(st + 4 * (lane + 64), mask_tail(R.g1, g.sb + 16 * (lane + 64), S.n));
-  if (lane + 128 < g.ng) sts16(st + 4 * (lane + 128), mask_tail(R.g2, g.sb + 16 * (lane + 128), S.n));
-  __builtin_amdgcn_wave_barrier();
-  const uint32_t i0 = g.v0 + lane * 8;
-  if (i0 < g.v1) {
-    const int cnt = (int)(g.v1 - i0 < 8 ? g.v1 - i0 : 8);
-    int lo = 0, hi = (int)g.nr - 1;  // last run with start <= i0
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (run_start(sh.runs[mid]) <= i0) lo = mid; else hi = mid - 1;
-    }
-    int r = lo;
-    RunEnt cur = sh.runs[r];
-    uint32_t nxt = r + 1 < (int)g.nr ? run_start(sh.runs[r + 1]) : 0xffffffffu;
-    uint32_t v[8];
+// Decode this lane's 8 values of block b (after install): the run of value i
+// is the last run starting at or before i.  Runs mark their first value in
+// rmap, a wave-wide prefix max turns the marks into a run index per value, so
+// no lane walks runs one by one (a divergent, serial LDS chain).
+__device__ __forceinline__ void block_values(const ExpandShared& sh, int b, const BlockGeom& g, uint32_t mask, int w,
+                                             int lane, uint32_t (&v)[8]) {
+  // marks of this lane's 8 values (written before the caller's barrier)
+  const u32x2_t mk = *(const PQG_L u32x2_t*)(lds_ptr(sh.rmap[b]) + 8 * lane);
+  uint32_t idx[8];
+  uint32_t run_max = 0;
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const uint32_t i = i0 + q;
-      v[q] = 0;
-      if (q < cnt) {
-        while (i >= nxt) {
-          r++;
-          cur = sh.runs[r];
-          nxt = r + 1 < (int)g.nr ? run_start(sh.runs[r + 1]) : 0xffffffffu;
-        }
-        if (!(cur.start & kRunBP)) {
-          v[q] = cur.src;
-        } else {
-          const int64_t rb = (int64_t)cur.src * 8 + (int64_t)(i - run_start(cur)) * w - g.sb * 8;
-          const int d = (int)(rb >> 5);
-          const uint32_t lo32 = sh.stage[d], hi32 = sh.stage[d + 1];
-          v[q] = __builtin_amdgcn_alignbit(hi32, lo32, (uint32_t)rb & 31) & mask;
-        }
-      }
+  for (int q = 0; q < 8; q++) {
+    const uint32_t m = ((q < 4 ? mk.x : mk.y) >> (8 * (q & 3))) & 0xff;
+    run_max = m > run_max ? m : run_max;
+    idx[q] = run_max;
+  }
+  // exclusive prefix max of the lanes' maxima
+  uint32_t incl = run_max;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl = t > incl ? t : incl;
+  }
+  uint32_t before = __shfl_up(incl, 1, 64);
+  if (lane == 0) before = 0;
+  const int64_t sb8 = g.sb * 8;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint32_t r = idx[q] > before ? idx[q] : before;
+    const RunEnt e = sh.runs[b][r];
+    const uint32_t i = g.v0 + lane * 8 + q;
+    if (!(e.start & kRunBP)) {
+      v[q] = e.src;
+    } else {
+      const uint32_t rb = (uint32_t)((int64_t)e.src * 8 - sb8) + (i - run_start(e)) * (uint32_t)w;
+      const uint32_t d = rb >> 5;
+      v[q] = __builtin_amdgcn_alignbit(sh.stage[b][d + 1], sh.stage[b][d], rb & 31) & mask;
     }
-    sink.put(i0, v, cnt);
   }
 }
 
-// Sink: void put(uint32_t i0, const uint32_t (&v)[8], int cnt)  (cnt <= 8 values from i0)
+// Sink:
+//   void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup], const int (&cnt)[kGroup])
+// values v[b][0..cnt[b]) belong at value indices i0[b]...; cnt[b] == 0: none.
 template <class Sink>
-__device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __restrict__ runs_, const BlockDesc* __restrict__ blks_,
-                              int64_t count, ExpandShared& sh, Sink& sink) {
+__device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __restrict__ runs_,
+                                              const BlockDesc* __restrict__ blks_, int64_t count, ExpandShared& sh,
+                                              Sink& sink) {
   const int lane = lane_id();
   const int w = S.w;
   const uint32_t mask = w == 32 ? 0xffffffffu : ((1u << w) - 1);
@@ -156,6 +130,7 @@ __device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __
   if (count <= 0) return;
   const uint32_t end_all = (uint32_t)count;
   const gcu8 sp = gconst(S.p);
+  const uintptr_t pa = (uintptr_t)S.p;
   const int64_t n = S.n;
   const PQG_G RunEnt* runs = gconst(runs_) + S.run_base;
   const PQG_G BlockDesc* blks = gconst(blks_) + S.blk_base;
@@ -175,27 +150,66 @@ __device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __
     int nk = nb;  // blocks starting at or past `count` are not needed
     while (nk > 0 && sh.desc[nk - 1].v0 >= end_all) nk--;
     if (nk == 0) break;
-    // values of the last block here end at the next batch's first block, or at count
+    // the last block here ends at the next batch's first block, or at count
     uint32_t tail_end = end_all;
     if (nk == nb && b0 + nb < nb_all) {
       const uint32_t nv0 = blks[b0 + nb].v0;
       tail_end = nv0 < end_all ? nv0 : end_all;
     }
-    BlockRegs A, B;
-    BlockGeom ga = block_geom(sh, 0, nk, tail_end, S), gb;
-    block_fetch(A, ga, runs, sp, n, lane);
-    for (int k = 0; k < nk; k += 2) {
-      if (k + 1 < nk) {
-        gb = block_geom(sh, k + 1, nk, tail_end, S);
-        block_fetch(B, gb, runs, sp, n, lane);
+    for (int k0 = 0; k0 < nk; k0 += kGroup) {
+      PQG_T(t0);
+      BlockGeom g[kGroup];
+      uint32_t rs[kGroup], rv[kGroup];
+      uint4 gr[kGroup];
+#pragma unroll
+      for (int b = 0; b < kGroup; b++) {
+        const int k = k0 + b < nk ? k0 + b : nk - 1;  // past the end: repeat the last block, unused
+        g[b] = block_geom(sh, k, nk, tail_end, pa);
+        const uint32_t ri = (uint32_t)lane < g[b].nr ? (uint32_t)lane : 0u;  // nr >= 1
+        rs[b] = runs[g[b].r0 + ri].start;
+        rv[b] = runs[g[b].r0 + ri].src;
+        // granule `lane`, if it holds a stream byte < n (mapped); else a safe address
+        const int64_t at = g[b].sb + 16 * lane;
+        const bool want = lane < g[b].ng && at < n;
+        gr[b] = ldg16(want ? (uintptr_t)(sp + at) : ((uintptr_t)(runs + g[b].r0) & ~(uintptr_t)15));
       }
-      block_process(A, ga, sh, S, mask, w, lane, sink);
-      if (k + 1 >= nk) break;
-      if (k + 2 < nk) {
-        ga = block_geom(sh, k + 2, nk, tail_end, S);
-        block_fetch(A, ga, runs, sp, n, lane);
+      PQG_T(t1);
+      PQG_ACC(0, t0, t1);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int b = 0; b < kGroup; b++) {
+        *(PQG_L u32x2_t*)(lds_ptr(sh.rmap[b]) + 8 * lane) = u32x2_t{0u, 0u};
+        if ((uint32_t)lane < g[b].nr) {
+          sh.runs[b][lane].start = rs[b];
+          sh.runs[b][lane].src = rv[b];
+        }
+        if (lane < g[b].ng) sts16(lds_ptr(sh.stage[b]) + 4 * lane, mask_tail(gr[b], g[b].sb + 16 * lane, n));
       }
-      block_process(B, gb, sh, S, mask, w, lane, sink);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int b = 0; b < kGroup; b++) {
+        // run r > 0 starts inside the block (run 0 holds value v0)
+        if (lane > 0 && (uint32_t)lane < g[b].nr) sh.rmap[b][(rs[b] & ~kRunBP) - g[b].v0] = (uint8_t)lane;
+      }
+      __builtin_amdgcn_wave_barrier();
+      PQG_T(t2);
+      PQG_ACC(1, t1, t2);
+      uint32_t v[kGroup][8], i0[kGroup];
+      int cnt[kGroup];
+#pragma unroll
+      for (int b = 0; b < kGroup; b++) {
+        i0[b] = g[b].v0 + lane * 8;
+        cnt[b] = (k0 + b < nk && i0[b] < g[b].v1) ? (int)(g[b].v1 - i0[b] < 8 ? g[b].v1 - i0[b] : 8) : 0;
+        block_values(sh, b, g[b], mask, w, lane, v[b]);
+      }
+      PQG_T(t3);
+      PQG_ACC(2, t2, t3);
+      sink.group(v, i0, cnt);
+      PQG_T(t4);
+      PQG_ACC(3, t3, t4);
+#ifdef PQG_PROFILE
+      if (lane == 0) atomicAdd(&pqg_prof[4], 1ull);
+#endif
     }
   }
   __builtin_amdgcn_wave_barrier();

@@ -26,11 +26,22 @@
 
 namespace pqg {
 
+#ifdef PQG_PROFILE
+// host reader of this translation unit's phase counters (see pqg_debug_counters)
+int prof_read_levels(unsigned long long* out) {
+  unsigned long long z[64] = {0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pqg_prof), sizeof(z)) != hipSuccess) return -1;
+  hipMemcpyToSymbol(HIP_SYMBOL(pqg_prof), z, sizeof(z));
+  return 0;
+}
+#endif
+
 // ---- K3a ---------------------------------------------------------------------
 __device__ __forceinline__ int reg_stream(JobDev& job, HStream* streams, int32_t* slot, int pidx, int kind,
                                           gcu8 p, int64_t n, int w, int64_t count) {
   const int64_t nruns = n / 2 + 2;  // every run but a truncated last one takes >= 2 bytes
-  const int64_t nblks = count / kHBlock + nruns / kHBlockRuns + 2;  // blocks close at kHBlock values or kHBlockRuns runs
+  // blocks close at kHBlock values, kHBlockRuns runs or kHBlockBytes payload bytes
+  const int64_t nblks = count / kHBlock + nruns / kHBlockRuns + n / (kHBlockBytes / 2) + 3;
   const int64_t rb = (int64_t)atomicAdd((unsigned long long*)&job.run_used, (unsigned long long)nruns);
   const int64_t bb = (int64_t)atomicAdd((unsigned long long*)&job.blk_used, (unsigned long long)nblks);
   if (rb + nruns > job.run_cap || bb + nblks > job.blk_cap) {
@@ -56,7 +67,8 @@ __device__ __forceinline__ int reg_stream(JobDev& job, HStream* streams, int32_t
 }
 
 __global__ void __launch_bounds__(256) k_page_setup(JobDev* jobs, PageDev* pages, const int* list, const int* total,
-                                                    uint8_t* scratch, HStream* streams) {
+                                                    uint8_t* scratch, HStream* streams, int* vlists, int* vcount,
+                                                    int list_cap) {
   const int nt = *total;
   for (int t = blockIdx.x * 256 + threadIdx.x; t < nt; t += gridDim.x * 256) {
     const int pidx = list[t];
@@ -141,6 +153,10 @@ __global__ void __launch_bounds__(256) k_page_setup(JobDev* jobs, PageDev* pages
       const int64_t take = min(sz, vn - 4);
       if (n > 0) reg_stream(job, streams, &pg.hs_val, pidx, 3, val + 4, take, 1, n);
     }
+    // value-stage page lists: 4-byte dictionary pages (the hot path, a kernel
+    // of its own) and everything else
+    const int mode = (pg.encoding == 8 && job.value_width == 4) ? 1 : 0;
+    vlists[mode * list_cap + atomicAdd(&vcount[mode], 1)] = pidx;
   }
 }
 
@@ -315,14 +331,29 @@ __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pag
             blo = ~0ull;
             bhi = 0;
           }
-          bn++;
-          const uint32_t pe = rend < bv0 + kHBlock ? rend : bv0 + kHBlock;
+          uint32_t pe = rend < bv0 + kHBlock ? rend : bv0 + kHBlock;
           if (st & kRunBP) {
-            const uint64_t b0 = ((uint64_t)src * 8 + (uint64_t)(v - produced) * w) >> 3;
-            const uint64_t b1 = ((uint64_t)src * 8 + (uint64_t)(pe - produced) * w + 7) >> 3;
-            blo = b0 < blo ? b0 : blo;
+            const uint64_t rbit = (uint64_t)src * 8;  // bit of the run's value 0
+            const uint64_t b0 = (rbit + (uint64_t)(v - produced) * w) >> 3;
+            const uint64_t org = blo < b0 ? blo : b0;
+            // values whose bits end within org + kHBlockBytes
+            const uint64_t lim = (org + kHBlockBytes) * 8;
+            const uint64_t fit = lim > rbit ? (lim - rbit) / w : 0;  // values [0, fit) of the run fit
+            if (produced + fit <= v) {  // not even one more value: start a new block here
+              close_block();
+              bv0 = v;
+              br0 = nr;
+              bn = 0;
+              blo = ~0ull;
+              bhi = 0;
+              continue;
+            }
+            if (produced + fit < pe) pe = (uint32_t)(produced + fit);
+            const uint64_t b1 = (rbit + (uint64_t)(pe - produced) * w + 7) >> 3;
+            blo = org;
             bhi = b1 > bhi ? b1 : bhi;
           }
+          bn++;
           v = pe;
         }
         produced = rend;
@@ -343,14 +374,20 @@ struct LevelSink {
   gu8 out;
   uint32_t maxl;
   int64_t nn;
-  __device__ __forceinline__ void put(uint32_t i0, const uint32_t (&v)[8], int cnt) {
-    gu8 o = out + i0;
-    if (cnt == 8 && ((uintptr_t)o & 7) == 0) {
-      stg8((uintptr_t)o, v[0] | v[1] << 8 | v[2] << 16 | v[3] << 24, v[4] | v[5] << 8 | v[6] << 16 | v[7] << 24);
-    } else {
-      for (int q = 0; q < cnt; q++) o[q] = (uint8_t)v[q];
+  __device__ __forceinline__ void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup],
+                                        const int (&cnt)[kGroup]) {
+#pragma unroll
+    for (int b = 0; b < kGroup; b++) {
+      if (cnt[b] == 0) continue;
+      gu8 o = out + i0[b];
+      if (cnt[b] == 8 && ((uintptr_t)o & 7) == 0) {
+        stg8((uintptr_t)o, v[b][0] | v[b][1] << 8 | v[b][2] << 16 | v[b][3] << 24,
+             v[b][4] | v[b][5] << 8 | v[b][6] << 16 | v[b][7] << 24);
+      } else {
+        for (int q = 0; q < cnt[b]; q++) o[q] = (uint8_t)v[b][q];
+      }
+      for (int q = 0; q < cnt[b]; q++) nn += v[b][q] == maxl;
     }
-    for (int q = 0; q < cnt; q++) nn += v[q] == maxl;
   }
 };
 

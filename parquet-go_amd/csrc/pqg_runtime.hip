@@ -33,17 +33,25 @@ __global__ void k_page_list(JobDev* jobs, int n_jobs, int* list, int list_cap, i
 __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                          uint8_t* scratch);
 __global__ void k_page_setup(JobDev* jobs, PageDev* pages, const int* list, const int* total, uint8_t* scratch,
-                             HStream* streams);
+                             HStream* streams, int* vlists, int* vcount, int list_cap);
 __global__ void k_hybrid_walk(const PageDev* pages, const int* list, const int* total, HStream* streams,
                               RunEnt* runs, BlockDesc* blks);
 __global__ void k_levels_expand(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                                 const HStream* streams, const RunEnt* runs, const BlockDesc* blks, uint8_t* def_arena,
                                 uint8_t* rep_arena);
 __global__ void k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch);
+template <int Mode>
 __global__ void k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                          uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks);
 __global__ void k_finalize(JobDev* jobs, int n_jobs, PageDev* pages);
 }  // namespace pqg
+
+#ifdef PQG_PROFILE
+namespace pqg {
+int prof_read_values(unsigned long long* out);
+int prof_read_levels(unsigned long long* out);
+}  // namespace pqg
+#endif
 
 using namespace pqg;
 
@@ -98,7 +106,7 @@ struct pqg_ctx {
   DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
   DevBuf tile_count, tile_okc, tile_off, tile_okoff, cand_pos, cands, succ, idx2slot, ok2slot, order;  // K1
   DevBuf streams, runs, blks;  // K3 hybrid run tables
-  DevBuf cand_list;
+  DevBuf cand_list, vlists;
   int64_t total_tiles = 0;
   JobDev* h_jobs = nullptr;  // pinned
   int h_jobs_cap = 0;
@@ -165,7 +173,7 @@ void pqg_ctx_destroy(pqg_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (auto& e : c->ev) hipEventDestroy(e);
   for (DevBuf* b : {&c->jobs, &c->pages, &c->list, &c->counters, &c->def_arena, &c->rep_arena, &c->value_arena,
-                    &c->scratch, &c->streams, &c->runs, &c->blks, &c->cand_list, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
+                    &c->scratch, &c->streams, &c->runs, &c->blks, &c->cand_list, &c->vlists, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
                     &c->ok2slot, &c->order})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
@@ -257,7 +265,7 @@ static int plan_batch(pqg_ctx* c) {
     d.run_cap = rcap;
     d.run_base = run_total;
     run_total += rcap;
-    int64_t bcap = 3 * (scap / kHBlock + 2 * pcap) + rcap / kHBlockRuns + 64;
+    int64_t bcap = 3 * (scap / kHBlock + 3 * pcap) + rcap / kHBlockRuns + 2 * rcap / (kHBlockBytes / 2) + 64;
     if (c->force_blks[(size_t)i] > 0) bcap = c->force_blks[(size_t)i];
     d.blk_cap = bcap;
     d.blk_base = blk_total;
@@ -278,6 +286,7 @@ static int plan_batch(pqg_ctx* c) {
       c->ok2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->cand_pos.grow(sizeof(int64_t) * (size_t)tile_total * kCandPerTile + 64) ||
       c->cand_list.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
+      c->vlists.grow(sizeof(int) * 2 * (size_t)page_total + 64) ||
       c->cands.grow(sizeof(Cand) * (size_t)tile_total * kCandPerTile + 64) ||
       c->succ.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->idx2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
@@ -337,7 +346,10 @@ static int launch_pipeline(pqg_ctx* c) {
   RunEnt* runs = (RunEnt*)c->runs.p;
   BlockDesc* blks = (BlockDesc*)c->blks.p;
   const unsigned lane_blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((c->list_cap + 255) / 256, c->num_cus * 4));
-  hipLaunchKernelGGL(k_page_setup, dim3(lane_blocks), dim3(256), 0, s, jobs, pages, list, ctr, scratch, streams);
+  int* vlists = (int*)c->vlists.p;
+  const int lcap = (int)std::min<int64_t>(c->list_cap, INT32_MAX);
+  hipLaunchKernelGGL(k_page_setup, dim3(lane_blocks), dim3(256), 0, s, jobs, pages, list, ctr, scratch, streams, vlists,
+                     ctr + 12, lcap);
   if (c->timed) hipEventRecord(c->ev[4], s);
   const unsigned walk_blocks =
       (unsigned)std::max<int64_t>(1, std::min<int64_t>((3 * c->list_cap + 255) / 256, c->num_cus * 8));
@@ -348,7 +360,9 @@ static int launch_pipeline(pqg_ctx* c) {
   if (c->timed) hipEventRecord(c->ev[6], s);
   hipLaunchKernelGGL(k_nn_scan, dim3(n), dim3(256), 0, s, jobs, pages, scratch);
   if (c->timed) hipEventRecord(c->ev[7], s);
-  hipLaunchKernelGGL(k_values, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 10,
+  hipLaunchKernelGGL(k_values<1>, dim3(waves), dim3(64), 0, s, jobs, pages, vlists + lcap, ctr + 13, ctr + 11,
+                     (uint8_t*)c->value_arena.p, streams, runs, blks);
+  hipLaunchKernelGGL(k_values<0>, dim3(waves), dim3(64), 0, s, jobs, pages, vlists, ctr + 12, ctr + 10,
                      (uint8_t*)c->value_arena.p, streams, runs, blks);
   if (c->timed) hipEventRecord(c->ev[8], s);
   hipLaunchKernelGGL(k_finalize, dim3(n), dim3(256), 0, s, jobs, n, pages);
@@ -470,6 +484,23 @@ int pqg_get_pages(pqg_ctx* c, int job, pqg_page_info* out, int cap) {
     o.flags = p.flags;
   }
   return k;
+}
+
+// Diagnostic builds (-DPQG_PROFILE): in-kernel phase cycle counters of the
+// values (slots 0-31) and levels (slots 32-63) translation units; read + reset.
+int pqg_debug_counters(pqg_ctx* c, uint64_t* out, int cap) {
+  if (!c || !out) return PQG_ERR_INVALID_ARG;
+#ifdef PQG_PROFILE
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  unsigned long long a[64], b[64];
+  if (pqg::prof_read_values(a) || pqg::prof_read_levels(b)) return PQG_ERR_HIP;
+  int k = 0;
+  for (; k < 64 && k < cap; k++) out[k] = k < 32 ? a[k] : b[k - 32];
+  return k;
+#else
+  return 0;
+#endif
 }
 
 int pqg_debug_job(pqg_ctx* c, int job, int64_t* out, int cap) {

@@ -16,59 +16,83 @@
 
 namespace pqg {
 
+#ifdef PQG_PROFILE
+// host reader of this translation unit's phase counters (see pqg_debug_counters)
+int prof_read_values(unsigned long long* out) {
+  unsigned long long z[64] = {0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pqg_prof), sizeof(z)) != hipSuccess) return -1;
+  hipMemcpyToSymbol(HIP_SYMBOL(pqg_prof), z, sizeof(z));
+  return 0;
+}
+#endif
+
 // ============================================================================
 // K4: values — one wave per data page.
 // ============================================================================
 // dictDecoder.decodeValues (type_dict.go:39-59): dst[i] = values[key],
-// "dict: invalid index" when key >= len(values).  W bytes per entry.
+// "dict: invalid index" when key >= len(values).  W bytes per entry (W == 0:
+// runtime width `w`, a byte-copy path for FLBA / INT96 dictionaries).  All the
+// gathers of a group are issued before its stores (see pqg_hybrid.h).
 template <int W>
 struct DictSink {
   gu8 out;
-  gcu8 dict;
+  gcu8 dict;        // never null (a safe base when the chunk has no dictionary)
   int64_t count;
   int64_t bad;      // first index with an invalid key
   int64_t nil_key;  // INT96 partial final entry (-1: none): its value reads as zero bytes (Q8)
-  int w;            // entry width when W == 0
-  __device__ __forceinline__ void put(uint32_t i0, const uint32_t (&v)[8], int cnt) {
-    bool ok = true;
-    for (int q = 0; q < cnt; q++)
-      if ((int64_t)v[q] >= count) {
-        ok = false;
-        bad = i0 + q < bad ? i0 + q : bad;
+  int w;
+  __device__ __forceinline__ void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup],
+                                        const int (&cnt)[kGroup]) {
+    bool ok[kGroup][8];
+#pragma unroll
+    for (int b = 0; b < kGroup; b++)
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        ok[b][q] = q < cnt[b] && (int64_t)v[b][q] < count;
+        if (q < cnt[b] && !ok[b][q]) bad = (int64_t)(i0[b] + q) < bad ? (int64_t)(i0[b] + q) : bad;
       }
-    if (W == 4 && ok && cnt == 8 && ((uintptr_t)(out + i0 * 4) & 15) == 0) {
+    if (W == 4) {
+      uint32_t gv[kGroup][8];
       const PQG_G uint32_t* d = (const PQG_G uint32_t*)dict;
-      const uint4 a = make_uint4(d[v[0]], d[v[1]], d[v[2]], d[v[3]]);
-      const uint4 b = make_uint4(d[v[4]], d[v[5]], d[v[6]], d[v[7]]);
-      stg16((uintptr_t)(out + i0 * 4), a);
-      stg16((uintptr_t)(out + i0 * 4 + 16), b);
-      return;
-    }
-    if (W == 8 && ok && cnt == 8 && ((uintptr_t)(out + i0 * 8) & 15) == 0) {
+#pragma unroll
+      for (int b = 0; b < kGroup; b++)
+#pragma unroll
+        for (int q = 0; q < 8; q++) gv[b][q] = d[ok[b][q] ? v[b][q] : 0u];
+#pragma unroll
+      for (int b = 0; b < kGroup; b++) {
+        if (cnt[b] == 0) continue;
+        const uintptr_t o = (uintptr_t)(out + (int64_t)i0[b] * 4);
+        if (cnt[b] == 8 && (o & 15) == 0 && ok[b][0] && ok[b][1] && ok[b][2] && ok[b][3] && ok[b][4] && ok[b][5] &&
+            ok[b][6] && ok[b][7]) {
+          stg16(o, make_uint4(gv[b][0], gv[b][1], gv[b][2], gv[b][3]));
+          stg16(o + 16, make_uint4(gv[b][4], gv[b][5], gv[b][6], gv[b][7]));
+        } else {
+          for (int q = 0; q < cnt[b]; q++)
+            if (ok[b][q]) ((PQG_G uint32_t*)o)[q] = gv[b][q];
+        }
+      }
+    } else if (W == 8) {
+      u32x2_t gv[kGroup][8];
       const PQG_G u32x2_t* d = (const PQG_G u32x2_t*)dict;
 #pragma unroll
-      for (int q = 0; q < 8; q += 2) {
-        const u32x2_t x = d[v[q]], y = d[v[q + 1]];
-        stg16((uintptr_t)(out + i0 * 8 + q * 8), make_uint4(x.x, x.y, y.x, y.y));
+      for (int b = 0; b < kGroup; b++)
+#pragma unroll
+        for (int q = 0; q < 8; q++) gv[b][q] = d[ok[b][q] ? v[b][q] : 0u];
+#pragma unroll
+      for (int b = 0; b < kGroup; b++) {
+        if (cnt[b] == 0) continue;
+        const uintptr_t o = (uintptr_t)(out + (int64_t)i0[b] * 8);
+        for (int q = 0; q < cnt[b]; q++)
+          if (ok[b][q]) stg8(o + 8 * q, gv[b][q].x, gv[b][q].y);
       }
-      return;
-    }
-    const int ww = W > 0 ? W : w;
-    for (int q = 0; q < cnt; q++) {
-      const int64_t key = v[q];
-      if (key >= count) continue;
-      const int64_t i = i0 + q;
-      if (W == 4) {
-        *(PQG_G uint32_t*)(out + i * 4) = *(const PQG_G uint32_t*)(dict + key * 4);
-      } else if (W == 8) {
-        const PQG_G uint32_t* s = (const PQG_G uint32_t*)(dict + key * 8);
-        PQG_G uint32_t* d = (PQG_G uint32_t*)(out + i * 8);
-        d[0] = s[0];
-        d[1] = s[1];
-      } else {
-        gcu8 s = dict + key * ww;
-        for (int b = 0; b < ww; b++) out[i * ww + b] = (key == nil_key) ? 0 : s[b];
-      }
+    } else {
+      for (int b = 0; b < kGroup; b++)
+        for (int q = 0; q < cnt[b]; q++) {
+          if (!ok[b][q]) continue;
+          const int64_t key = v[b][q], i = (int64_t)i0[b] + q;
+          gcu8 s = dict + key * w;
+          for (int c = 0; c < w; c++) out[i * w + c] = (key == nil_key) ? 0 : s[c];
+        }
     }
   }
 };
@@ -76,8 +100,10 @@ struct DictSink {
 // booleanRLEDecoder (type_boolean.go:100-120): value == 1
 struct BoolSink {
   gu8 out;
-  __device__ __forceinline__ void put(uint32_t i0, const uint32_t (&v)[8], int cnt) {
-    for (int q = 0; q < cnt; q++) out[i0 + q] = v[q] == 1;
+  __device__ __forceinline__ void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup],
+                                        const int (&cnt)[kGroup]) {
+    for (int b = 0; b < kGroup; b++)
+      for (int q = 0; q < cnt[b]; q++) out[i0[b] + q] = v[b][q] == 1;
   }
 };
 
@@ -315,12 +341,17 @@ union ValuesShared {
   DbpShared dbp;
 };
 
+// Mode 1: pages of 4-byte dictionary columns only (the C2 hot path, kept
+// apart so that its register budget is not the union of every encoding's);
+// mode 0: every other data page.  k_page_setup builds the two page lists.
+template <int Mode>
 __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total,
                                                int* queue, uint8_t* value_arena, const HStream* streams,
                                                const RunEnt* runs, const BlockDesc* blks) {
   __shared__ __attribute__((aligned(16))) ValuesShared sh;
   const int lane = lane_id();
   for (;;) {
+    PQG_T(tp0);
     const int t = queue_next(queue);
     if (t >= *total) return;
     // wave-uniform: page and job records are read once, by scalar loads, into
@@ -336,6 +367,8 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
     int64_t readable = (pg.scratch_offset >= 0) ? vn : job.data_len - (pg.val - job.data);
     const int enc = pg.encoding;
     const int64_t nn = pg.not_null;
+    PQG_T(tpa);
+    PQG_ACC(10 + Mode, tp0, tpa);
     const int w = job.value_width;
     const gu8 out = gmut(value_arena) + job.value_base + pg.value_offset * (int64_t)w;
     // ---- valuesDecoder.init (read phase)
@@ -347,9 +380,9 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
         dict_w = val[0];
         if (dict_w > 32) re = kBIT_WIDTH;
       }
-    } else if (enc == 5) {
+    } else if (Mode == 0 && enc == 5) {
       re = dbp_decode(val, vn, readable, job.type == 2, 0, nullptr, sh.dbp, 0);
-    } else if (enc == 3 && job.type == 0) {
+    } else if (Mode == 0 && enc == 3 && job.type == 0) {
       if (vn < 4) re = kEOF;
     }
     if (re != kOK) {
@@ -359,7 +392,7 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
     if (pg.decode_status != kOK || nn == 0) continue;
     // ---- decodeValues(val[:nn]) (decode phase)
     int de = kOK;
-    if (enc == 0) {
+    if (Mode == 0 && enc == 0) {
       if (job.type == 0) {  // booleanPlainDecoder: one byte per 8 values
         if ((nn + 7) / 8 > vn) de = kEOF;
         else
@@ -407,25 +440,26 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
         const HStream S = streams[pg.hs_val];
         const int serr = (S.status != kOK && S.produced < nn) ? S.status : kOK;
         int64_t bad = nn;
-        if (w == 4) {
-          DictSink<4> sk{out, dict, dcount, nn, nil_key, 4};
+        const gcu8 dsafe = dict ? dict : (gcu8)out;  // never dereferenced for a valid key when null
+        if (Mode == 1 || w == 4) {
+          DictSink<4> sk{out, dsafe, dcount, nn, nil_key, 4};
           hybrid_expand(S, runs, blks, nn, sh.ex, sk);
           bad = wave_min(sk.bad);
-        } else if (w == 8) {
-          DictSink<8> sk{out, dict, dcount, nn, nil_key, 8};
+        } else if (Mode == 0 && w == 8) {
+          DictSink<8> sk{out, dsafe, dcount, nn, nil_key, 8};
           hybrid_expand(S, runs, blks, nn, sh.ex, sk);
           bad = wave_min(sk.bad);
-        } else {
-          DictSink<0> sk{out, dict, dcount, nn, nil_key, w};
+        } else if (Mode == 0) {
+          DictSink<0> sk{out, dsafe, dcount, nn, nil_key, w};
           hybrid_expand(S, runs, blks, nn, sh.ex, sk);
           bad = wave_min(sk.bad);
         }
         if (bad < nn && (serr == kOK || bad < S.produced)) de = kDICT_INDEX;
         else de = serr;
       }
-    } else if (enc == 5) {
+    } else if (Mode == 0 && enc == 5) {
       de = dbp_decode(val, vn, readable, job.type == 2, nn, out, sh.dbp, 1);
-    } else if (enc == 3 && job.type == 0) {  // booleanRLEDecoder: hybrid w=1 after a u32 length
+    } else if (Mode == 0 && enc == 3 && job.type == 0) {  // booleanRLEDecoder: hybrid w=1 after a u32 length
       const HStream S = streams[pg.hs_val];
       BoolSink sk{out};
       hybrid_expand(S, runs, blks, nn, sh.ex, sk);
@@ -434,8 +468,15 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
       de = kUNSUPPORTED;
     }
     if (lane == 0 && de != kOK) pages[pidx].decode_status = de;
+    PQG_T(tp1);
+    PQG_ACC(8 + Mode, tp0, tp1);
   }
 }
+
+template __global__ void k_values<0>(JobDev*, PageDev*, const int*, const int*, int*, uint8_t*, const HStream*,
+                                    const RunEnt*, const BlockDesc*);
+template __global__ void k_values<1>(JobDev*, PageDev*, const int*, const int*, int*, uint8_t*, const HStream*,
+                                    const RunEnt*, const BlockDesc*);
 
 // ============================================================================
 // K5: chunk status in reference order (readPages errors first, then

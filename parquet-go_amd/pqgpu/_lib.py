@@ -6,6 +6,8 @@ from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(HERE), "csrc", "libpqgpu.so")
+# diagnostics only: PQG_LIB may name the -DPQG_PROFILE build (libpqgpu_prof.so)
+LIB_PATH = os.environ.get("PQG_LIB", LIB_PATH)
 
 _lib = None
 
@@ -34,6 +36,7 @@ def lib():
         "pqg_get_pages": ([P, I, C.POINTER(abi.PageInfo), I], I),
         "pqg_last_timings": ([P, C.POINTER(C.c_float), I], I),
         "pqg_debug_job": ([P, I, C.POINTER(I64), I], I),
+        "pqg_debug_counters": ([P, C.POINTER(C.c_uint64), I], I),
         "pqg_bench_decode": ([P, C.POINTER(abi.ChunkJob), I, I, C.POINTER(C.c_float), C.POINTER(C.c_float), I], I),
         "pqg_file_open": ([C.c_char_p, I64, C.POINTER(P)], I),
         "pqg_file_close": ([P], None),
@@ -55,7 +58,7 @@ def lib():
 EXPORTED = [
     "pqg_ctx_create", "pqg_ctx_destroy", "pqg_status_string", "pqg_device_alloc", "pqg_device_free",
     "pqg_memcpy_h2d", "pqg_memcpy_d2h", "pqg_decode_chunks_async", "pqg_sync", "pqg_decode_chunks",
-    "pqg_get_pages", "pqg_last_timings", "pqg_debug_job", "pqg_bench_decode", "pqg_file_open", "pqg_file_close",
+    "pqg_get_pages", "pqg_last_timings", "pqg_debug_job", "pqg_debug_counters", "pqg_bench_decode", "pqg_file_open", "pqg_file_close",
     "pqg_file_num_columns", "pqg_file_num_row_groups", "pqg_file_num_rows", "pqg_file_row_group_rows",
     "pqg_file_column", "pqg_file_chunk",
 ]
