@@ -40,6 +40,19 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def pmc_traffic(kernel, args):
+    """HBM bytes per launch of `kernel` from the committed PMC passes
+    (profiles/r01_pmc_traffic.json, made by tools/pmc_traffic.py from two
+    rocprofv3 --pmc runs of this same workload), or None for other workloads."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_traffic.json")
+    if args.rows != 100_000_000 or args.bits != "1,2,4,8,12,16,20" or not os.path.exists(path):
+        return None
+    ks = json.load(open(path))["kernels"]
+    # the values stage is k_values<1> (4-byte dictionaries) + k_values<0> (all else)
+    names = [k for k in ks if k.split("<")[0] == "pqg::" + kernel]
+    return sum(ks[k]["traffic"] for k in names) or None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -221,7 +234,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": pmc_traffic("k_" + dom_name, args),
                 "alg_bytes_per_launch": dom_bytes,
                 "kernel_ms": round(float(stage_ms[dom]), 4),
                 "pipeline_device_ms": round(dev_ms, 4),

@@ -223,6 +223,36 @@ int pqg_debug_job(pqg_ctx* ctx, int job, int64_t* out, int cap);
  * counters written (0 in normal builds). */
 int pqg_debug_counters(pqg_ctx* ctx, uint64_t* out, int cap);
 
+/* ---- K8: level assembly (null scatter / record and list offsets) ----------
+ * Replaces the per-slot cursor walk of ColumnStore.get (data_store.go:158-203)
+ * and Column.getData (schema.go:235-264): a slot with dLevel < maxD is a null
+ * (level cursor advances, value cursor does not); a slot with rLevel <
+ * maxR ends the current repeated object.  Evaluated for every slot at once:
+ *   valid(i)    = def[i] == max_def          (def_levels NULL → all valid)
+ *   boundary(i) = rep[i] <= boundary_level   (rep_levels NULL → every slot)
+ * boundary_level 0 = record starts (rLevel 0 → new row); max_rep-1 = the
+ * objects ColumnStore.get returns.  All pointers are DEVICE pointers (e.g. a
+ * pqg_chunk_result's def_levels/rep_levels/values); any output may be NULL. */
+typedef struct pqg_assemble_args {
+  const uint8_t* def_levels; /* num_slots bytes or NULL                          */
+  const uint8_t* rep_levels; /* num_slots bytes or NULL                          */
+  const uint8_t* values;     /* dense fixed-width values (num_valid × width)     */
+  int64_t num_slots;
+  int32_t max_def;
+  int32_t boundary_level;
+  int32_t value_width;       /* bytes per value; needed when values_spaced set   */
+  int32_t reserved;
+  uint8_t* validity;         /* out: ceil(num_slots/8) bytes, LSB-first bits     */
+  uint8_t* values_spaced;    /* out: num_slots × value_width, nulls zeroed       */
+  int64_t* offsets;          /* out: num_boundaries+1 entries (cap num_slots+1)  */
+  int64_t num_valid;         /* out: #valid slots (= notNull total)              */
+  int64_t null_count;        /* out: num_slots - num_valid                       */
+  int64_t num_boundaries;    /* out: #boundary slots (rows / objects)            */
+} pqg_assemble_args;
+
+/* Enqueue K8 on the ctx stream and wait; fills the three counts. */
+int pqg_assemble(pqg_ctx* ctx, pqg_assemble_args* args);
+
 /* ---- host-side planner: footer / schema (file_meta.go:14-62, schema.go) --- */
 typedef struct pqg_file pqg_file;
 

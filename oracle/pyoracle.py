@@ -34,6 +34,7 @@ def lib():
         L.pqo_snappy_decode.argtypes = [C.c_char_p, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
         L.pqo_delta_decode64.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_void_p]
         L.pqo_delta_decode32.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_void_p]
+        L.pqo_assemble.argtypes = [C.POINTER(abi.AssembleArgs)]
         _lib = L
     return _lib
 
@@ -105,3 +106,25 @@ def decode_chunk(job: abi.ChunkJob, page_cap: int = 1 << 20) -> OracleChunk:
                       res.value_width)
     L.pqo_free_result(C.byref(res))
     return out
+
+
+def assemble(def_levels, rep_levels, values, max_def, boundary_level, value_width):
+    """K8 oracle (ColumnStore.get cursor walk): returns (validity, spaced, offsets, counts)."""
+    n = len(def_levels) if def_levels is not None else len(rep_levels)
+    d = None if def_levels is None else np.ascontiguousarray(def_levels, dtype=np.uint8)
+    r = None if rep_levels is None else np.ascontiguousarray(rep_levels, dtype=np.uint8)
+    v = np.ascontiguousarray(values if values is not None else np.zeros(1, np.uint8)).view(np.uint8)
+    validity = np.zeros(max((n + 7) // 8, 1), np.uint8)
+    spaced = np.zeros(max(n * value_width, 1), np.uint8)
+    offsets = np.zeros(n + 1, np.int64)
+    a = abi.AssembleArgs()
+    a.def_levels = d.ctypes.data if d is not None else None
+    a.rep_levels = r.ctypes.data if r is not None else None
+    a.values = v.ctypes.data
+    a.num_slots, a.max_def, a.boundary_level, a.value_width = n, max_def, boundary_level, value_width
+    a.validity, a.values_spaced, a.offsets = validity.ctypes.data, spaced.ctypes.data if value_width else None, \
+        offsets.ctypes.data
+    rc = lib().pqo_assemble(C.byref(a))
+    assert rc == 0
+    return (validity[:(n + 7) // 8], spaced[:n * value_width], offsets[:a.num_boundaries + 1],
+            (a.num_valid, a.null_count, a.num_boundaries))

@@ -1,0 +1,183 @@
+// pqg_assemble.hip — K8: Dremel levels → validity bitmap, spaced values and
+// record/list offsets for one decoded column chunk.
+//
+// What it replaces: the per-slot walk of ColumnStore.get (data_store.go:158-203)
+// and Column.getData (schema.go:235-264).  There a slot with dLevel < maxD is a
+// null that advances the level cursor but not the value cursor; a slot with
+// rLevel < maxR ends the current repeated object.  Here the same two
+// predicates are evaluated for every slot at once:
+//   valid(i)    = def[i] == max_def                (def == NULL → all valid)
+//   boundary(i) = rep[i] <= boundary_level         (rep == NULL → every slot)
+// and the dense value cursor becomes rank(i) = #valid slots before i, so
+//   validity bit i      = valid(i)                 (LSB-first, Arrow layout)
+//   spaced[i]           = valid(i) ? dense[rank(i)] : 0
+//   offsets[#b before i]= i for every boundary slot, offsets[num_rows] = n.
+// boundary_level 0 gives record (row) starts (rep==0 → new row); maxR-1 gives
+// the objects ColumnStore.get returns (`rl < maxR` ends one).
+//
+// Three launches, all HBM-streaming integer work:
+//   k_asm_count  one wave per 4096-slot segment: ballot + popcount of both
+//                predicates (reads the level bytes once)
+//   k_asm_scan   one block: exclusive scan of the per-segment counts
+//   k_asm_write  one wave per segment again: 64 slots per ballot, the bitmap
+//                word is the ballot itself, ranks are popcount(mask & lt);
+//                value copies and stores are contiguous across the wave.
+#include <hip/hip_runtime.h>
+
+#include "pqgpu.h"
+#include "pqg_common.h"
+#include "pqg_device.h"
+
+namespace pqg {
+
+constexpr int kAsmSeg = 4096;  // slots per wave segment (64 ballots)
+
+__device__ __forceinline__ uint64_t ballot64(bool p) { return __ballot(p); }
+__device__ __forceinline__ int lane64() { return __lane_id(); }
+
+__device__ __forceinline__ bool slot_valid(const PQG_G uint8_t* def, int64_t i, int max_def) {
+  return def == nullptr || def[i] == (uint8_t)max_def;
+}
+__device__ __forceinline__ bool slot_boundary(const PQG_G uint8_t* rep, int64_t i, int level) {
+  return rep == nullptr || (int)rep[i] <= level;
+}
+
+__global__ void __launch_bounds__(256) k_asm_count(const uint8_t* def_, const uint8_t* rep_, int64_t n, int max_def,
+                                                   int level, int64_t nseg, int64_t* seg_cnt) {
+  const PQG_G uint8_t* def = gconst(def_);
+  const PQG_G uint8_t* rep = gconst(rep_);
+  const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (seg >= nseg) return;
+  const int lane = lane64();
+  const int64_t s0 = seg * kAsmSeg, s1 = s0 + kAsmSeg < n ? s0 + kAsmSeg : n;
+  int64_t nv = 0, nb = 0;
+  for (int64_t b = s0; b < s1; b += 64) {
+    const int64_t i = b + lane;
+    const bool in = i < s1;
+    nv += __popcll(ballot64(in && slot_valid(def, i, max_def)));
+    nb += __popcll(ballot64(in && slot_boundary(rep, i, level)));
+  }
+  if (lane == 0) {
+    PQG_G int64_t* o = gmut(seg_cnt) + 2 * seg;
+    o[0] = nv;
+    o[1] = nb;
+  }
+}
+
+// Exclusive scan of (valid, boundary) pairs in place; tot[0..1] = totals.
+// Writes offsets[num_rows] = n (the closing offset).
+__global__ void __launch_bounds__(1024) k_asm_scan(int64_t* seg_cnt, int64_t nseg, int64_t n, int64_t* tot,
+                                                   int64_t* offsets) {
+  __shared__ int64_t sv[1024], sb[1024];
+  __shared__ int64_t carry[2];
+  const int t = threadIdx.x;
+  if (t == 0) carry[0] = carry[1] = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < nseg; base += 1024) {
+    const int64_t k = base + t;
+    int64_t v = 0, b = 0;
+    if (k < nseg) {
+      v = seg_cnt[2 * k];
+      b = seg_cnt[2 * k + 1];
+    }
+    sv[t] = v;
+    sb[t] = b;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {  // Hillis–Steele inclusive scan
+      const int64_t av = t >= d ? sv[t - d] : 0, ab = t >= d ? sb[t - d] : 0;
+      __syncthreads();
+      sv[t] += av;
+      sb[t] += ab;
+      __syncthreads();
+    }
+    const int64_t cv = carry[0], cb = carry[1];
+    if (k < nseg) {
+      seg_cnt[2 * k] = cv + sv[t] - v;
+      seg_cnt[2 * k + 1] = cb + sb[t] - b;
+    }
+    __syncthreads();
+    if (t == 1023) {
+      carry[0] = cv + sv[t];
+      carry[1] = cb + sb[t];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    tot[0] = carry[0];
+    tot[1] = carry[1];
+    if (offsets) offsets[carry[1]] = n;
+  }
+}
+
+template <int W>
+__device__ __forceinline__ void copy_value(PQG_G uint8_t* dst, const PQG_G uint8_t* src, bool valid, int w) {
+  if constexpr (W == 4) {
+    *(PQG_G uint32_t*)dst = valid ? *(const PQG_G uint32_t*)src : 0u;
+  } else if constexpr (W == 8) {
+    *(PQG_G uint64_t*)dst = valid ? *(const PQG_G uint64_t*)src : 0ull;
+  } else if constexpr (W == 1) {
+    *dst = valid ? *src : (uint8_t)0;
+  } else {
+    for (int k = 0; k < w; k++) dst[k] = valid ? src[k] : (uint8_t)0;
+  }
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) k_asm_write(const uint8_t* def_, const uint8_t* rep_, const uint8_t* values_,
+                                                   int64_t n, int max_def, int level, int w, int64_t nseg,
+                                                   const int64_t* seg_cnt, uint8_t* validity_, uint8_t* spaced_,
+                                                   int64_t* offsets_) {
+  const PQG_G uint8_t* def = gconst(def_);
+  const PQG_G uint8_t* rep = gconst(rep_);
+  const PQG_G uint8_t* values = gconst(values_);
+  PQG_G uint8_t* validity = gmut(validity_);
+  PQG_G uint8_t* spaced = gmut(spaced_);
+  PQG_G int64_t* offsets = gmut(offsets_);
+  const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (seg >= nseg) return;
+  const int lane = lane64();
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const int64_t s0 = seg * kAsmSeg, s1 = s0 + kAsmSeg < n ? s0 + kAsmSeg : n;
+  const int64_t nbytes = (n + 7) >> 3;
+  int64_t rv = gconst(seg_cnt)[2 * seg], rb = gconst(seg_cnt)[2 * seg + 1];
+  for (int64_t b = s0; b < s1; b += 64) {
+    const int64_t i = b + lane;
+    const bool in = i < s1;
+    const bool v = in && slot_valid(def, i, max_def);
+    const bool bd = in && slot_boundary(rep, i, level);
+    const uint64_t mv = ballot64(v), mb = ballot64(bd);
+    if (validity && lane < 8 && (b >> 3) + lane < nbytes) validity[(b >> 3) + lane] = (uint8_t)(mv >> (8 * lane));
+    if (spaced && in) copy_value<W>(spaced + i * w, values + (rv + __popcll(mv & lt)) * w, v, w);
+    if (offsets && bd) offsets[rb + __popcll(mb & lt)] = i;
+    rv += __popcll(mv);
+    rb += __popcll(mb);
+  }
+}
+
+// Host launcher (called from pqg_assemble in pqg_runtime.hip).  seg_scratch
+// holds 2 × nseg int64; tot 2 int64 (device).
+int assemble_launch(hipStream_t s, const pqg_assemble_args* a, int64_t* seg_scratch, int64_t* tot) {
+  const int64_t n = a->num_slots;
+  const int64_t nseg = (n + kAsmSeg - 1) / kAsmSeg;
+  const unsigned blocks = (unsigned)((nseg + 3) / 4);
+  const int w = a->values_spaced ? a->value_width : 0;
+  if (nseg > 0)
+    hipLaunchKernelGGL(k_asm_count, dim3(blocks), dim3(256), 0, s, a->def_levels, a->rep_levels, n, a->max_def,
+                       a->boundary_level, nseg, seg_scratch);
+  hipLaunchKernelGGL(k_asm_scan, dim3(1), dim3(1024), 0, s, seg_scratch, nseg, n, tot, a->offsets);
+  if (nseg == 0) return hipGetLastError() == hipSuccess ? PQG_OK : PQG_ERR_HIP;
+#define PQG_ASM(WW)                                                                                                  \
+  hipLaunchKernelGGL(k_asm_write<WW>, dim3(blocks), dim3(256), 0, s, a->def_levels, a->rep_levels, a->values, n,    \
+                     a->max_def, a->boundary_level, w, nseg, (const int64_t*)seg_scratch, a->validity,              \
+                     a->values_spaced, a->offsets)
+  switch (w) {
+    case 1: PQG_ASM(1); break;
+    case 4: PQG_ASM(4); break;
+    case 8: PQG_ASM(8); break;
+    default: PQG_ASM(0); break;
+  }
+#undef PQG_ASM
+  return hipGetLastError() == hipSuccess ? PQG_OK : PQG_ERR_HIP;
+}
+
+}  // namespace pqg

@@ -18,6 +18,10 @@
 #include "pqg_common.h"
 
 namespace pqg {
+int assemble_launch(hipStream_t s, const pqg_assemble_args* a, int64_t* seg_scratch, int64_t* tot);  // pqg_assemble.hip
+}
+
+namespace pqg {
 __global__ void k_page_cands(JobDev* jobs, int n_jobs, int* tile_count, int* tile_okc, int64_t* cand_pos,
                              int* cand_list, int* cand_total);
 __global__ void k_cand_parse(JobDev* jobs, int n_jobs, const int* cand_list, const int* cand_total, int* tile_okc,
@@ -107,6 +111,7 @@ struct pqg_ctx {
   DevBuf tile_count, tile_okc, tile_off, tile_okoff, cand_pos, cands, succ, idx2slot, ok2slot, order;  // K1
   DevBuf streams, runs, blks;  // K3 hybrid run tables
   DevBuf cand_list, vlists;
+  DevBuf asm_seg;  // K8 per-segment counts + totals
   int64_t total_tiles = 0;
   JobDev* h_jobs = nullptr;  // pinned
   int h_jobs_cap = 0;
@@ -174,7 +179,7 @@ void pqg_ctx_destroy(pqg_ctx* c) {
   for (auto& e : c->ev) hipEventDestroy(e);
   for (DevBuf* b : {&c->jobs, &c->pages, &c->list, &c->counters, &c->def_arena, &c->rep_arena, &c->value_arena,
                     &c->scratch, &c->streams, &c->runs, &c->blks, &c->cand_list, &c->vlists, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
-                    &c->ok2slot, &c->order})
+                    &c->ok2slot, &c->order, &c->asm_seg})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
   hipStreamDestroy(c->stream);
@@ -439,6 +444,27 @@ int pqg_sync(pqg_ctx* c, pqg_chunk_result* results, int n_jobs) {
     r.values = (uint8_t*)c->value_arena.p + d.value_base;
     r.offsets = nullptr;
   }
+  return PQG_OK;
+}
+
+int pqg_assemble(pqg_ctx* c, pqg_assemble_args* a) {
+  if (!c || !a || a->num_slots < 0 || a->max_def < 0 || a->max_def > 255 || a->boundary_level < 0)
+    return PQG_ERR_INVALID_ARG;
+  if (a->values_spaced && (a->value_width <= 0 || (!a->values && a->num_slots > 0))) return PQG_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  const int64_t nseg = (a->num_slots + 4095) / 4096;
+  if (c->asm_seg.grow((size_t)(2 * nseg + 2) * sizeof(int64_t))) return PQG_ERR_HIP;
+  int64_t* seg = (int64_t*)c->asm_seg.p;
+  int64_t* tot = seg + 2 * nseg;
+  int e = pqg::assemble_launch(c->stream, a, seg, tot);
+  if (e) return e;
+  int64_t h[2] = {0, 0};
+  if (hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return PQG_ERR_HIP;
+  a->num_valid = h[0];
+  a->null_count = a->num_slots - h[0];
+  a->num_boundaries = h[1];
   return PQG_OK;
 }
 

@@ -124,5 +124,14 @@ class ChunkMeta(C.Structure):
     ]
 
 
+class AssembleArgs(C.Structure):
+    """pqg_assemble_args (include/pqgpu.h, K8)."""
+    _fields_ = [("def_levels", C.c_void_p), ("rep_levels", C.c_void_p), ("values", C.c_void_p),
+                ("num_slots", C.c_int64), ("max_def", C.c_int32), ("boundary_level", C.c_int32),
+                ("value_width", C.c_int32), ("reserved", C.c_int32),
+                ("validity", C.c_void_p), ("values_spaced", C.c_void_p), ("offsets", C.c_void_p),
+                ("num_valid", C.c_int64), ("null_count", C.c_int64), ("num_boundaries", C.c_int64)]
+
+
 def status_name(code):
     return STATUS.get(int(code), str(code))

@@ -175,6 +175,28 @@ class GpuDecoder:
         k = self.L.pqg_last_timings(self.ctx, out, 16)
         return [out[i] for i in range(max(k, 0))]
 
+    def assemble(self, def_ptr, rep_ptr, values_ptr, num_slots, max_def, boundary_level=0, value_width=0,
+                 validity=True, spaced=False, offsets=True):
+        """K8 on device arrays (e.g. a ChunkResult's levels/values): allocates the
+        requested outputs and returns (AssembleArgs, validity_ptr, spaced_ptr,
+        offsets_ptr).  Mirrors ColumnStore.get (data_store.go:158-203)."""
+        a = abi.AssembleArgs()
+        a.def_levels, a.rep_levels, a.values = def_ptr or None, rep_ptr or None, values_ptr or None
+        a.num_slots, a.max_def, a.boundary_level, a.value_width = num_slots, max_def, boundary_level, value_width
+
+        def alloc(nbytes):
+            p = C.c_void_p()
+            _check(self.L.pqg_device_alloc(self.ctx, max(nbytes, 1), C.byref(p)), "pqg_device_alloc")
+            self._bufs.append(p)
+            return p.value
+
+        vp = alloc((num_slots + 7) // 8) if validity else None
+        sp = alloc(num_slots * value_width) if spaced else None
+        op = alloc((num_slots + 1) * 8) if offsets else None
+        a.validity, a.values_spaced, a.offsets = vp, sp, op
+        _check(self.L.pqg_assemble(self.ctx, C.byref(a)), "pqg_assemble")
+        return a, vp, sp, op
+
     def download(self, r, job_index=None):
         lv_def = self.d2h(r.def_levels, r.num_slots) if (r.def_levels and r.status == 0) else None
         lv_rep = self.d2h(r.rep_levels, r.num_slots) if (r.rep_levels and r.status == 0) else None
