@@ -65,7 +65,8 @@ __global__ void __launch_bounds__(256) k_asm_count(const uint8_t* def_, const ui
 }
 
 // Exclusive scan of (valid, boundary) pairs in place; tot[0..1] = totals.
-// Writes offsets[num_rows] = n (the closing offset).
+// Writes offsets[num_rows] = n (the closing offset).  Each thread owns 4
+// consecutive segments, so one block-wide pass covers 4096 segments (16 M slots).
 __global__ void __launch_bounds__(1024) k_asm_scan(int64_t* seg_cnt, int64_t nseg, int64_t n, int64_t* tot,
                                                    int64_t* offsets) {
   __shared__ int64_t sv[1024], sb[1024];
@@ -73,32 +74,41 @@ __global__ void __launch_bounds__(1024) k_asm_scan(int64_t* seg_cnt, int64_t nse
   const int t = threadIdx.x;
   if (t == 0) carry[0] = carry[1] = 0;
   __syncthreads();
-  for (int64_t base = 0; base < nseg; base += 1024) {
-    const int64_t k = base + t;
-    int64_t v = 0, b = 0;
-    if (k < nseg) {
-      v = seg_cnt[2 * k];
-      b = seg_cnt[2 * k + 1];
+  for (int64_t base = 0; base < nseg; base += 4096) {
+    const int64_t k0 = base + 4 * (int64_t)t;
+    int64_t v[4], b[4], lv = 0, lb = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const bool in = k0 + j < nseg;
+      v[j] = in ? seg_cnt[2 * (k0 + j)] : 0;
+      b[j] = in ? seg_cnt[2 * (k0 + j) + 1] : 0;
+      lv += v[j];
+      lb += b[j];
     }
-    sv[t] = v;
-    sb[t] = b;
+    sv[t] = lv;
+    sb[t] = lb;
     __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {  // Hillis–Steele inclusive scan
+    for (int d = 1; d < 1024; d <<= 1) {  // Hillis–Steele inclusive scan of the per-thread sums
       const int64_t av = t >= d ? sv[t - d] : 0, ab = t >= d ? sb[t - d] : 0;
       __syncthreads();
       sv[t] += av;
       sb[t] += ab;
       __syncthreads();
     }
-    const int64_t cv = carry[0], cb = carry[1];
-    if (k < nseg) {
-      seg_cnt[2 * k] = cv + sv[t] - v;
-      seg_cnt[2 * k + 1] = cb + sb[t] - b;
+    int64_t ev = carry[0] + sv[t] - lv, eb = carry[1] + sb[t] - lb;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (k0 + j < nseg) {
+        seg_cnt[2 * (k0 + j)] = ev;
+        seg_cnt[2 * (k0 + j) + 1] = eb;
+      }
+      ev += v[j];
+      eb += b[j];
     }
     __syncthreads();
     if (t == 1023) {
-      carry[0] = cv + sv[t];
-      carry[1] = cb + sb[t];
+      carry[0] += sv[t];
+      carry[1] += sb[t];
     }
     __syncthreads();
   }

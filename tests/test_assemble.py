@@ -179,3 +179,13 @@ def test_gpu_assemble_decoded_chunks(dec):
                 dec.free(p)
         finally:
             dec.free(devp)
+
+
+@pytest.mark.gpu
+def test_gpu_assemble_multi_pass_scan(dec):
+    """> 4096 segments (16 M slots): the segment scan takes several block passes."""
+    rng = np.random.default_rng(77)
+    n = (1 << 24) + 3 * 4096 + 17
+    defs, reps, vals = _random_case(rng, n, 3, True, 4)
+    exp = O.assemble(defs, reps, vals, 3, 0, 4)
+    _check(_gpu_assemble(dec, defs, reps, vals, 3, 0, 4), exp)
