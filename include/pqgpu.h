@@ -134,7 +134,9 @@ typedef struct pqg_chunk_job {
 /* Decoded column chunk.  Fixed-width physical types (INT32/INT64/INT96/FLOAT/
  * DOUBLE/FLBA>0/BOOLEAN) store values densely, little endian, `value_width`
  * bytes each (BOOLEAN: one byte 0/1).  BYTE_ARRAY (and FLBA with length 0)
- * store chars in `values` and num_values+1 int64 offsets.  Pointers are DEVICE
+ * store the value bytes back to back in `values` (values_bytes = chars) and
+ * num_values+1 int64 `offsets` (offsets[0] = 0, value i = chars
+ * [offsets[i], offsets[i+1]); Arrow large-binary layout).  Pointers are DEVICE
  * pointers for libpqgpu (owned by the ctx, valid until the next decode on that
  * ctx or pqg_ctx_destroy) and malloc'ed host pointers for the oracle. */
 typedef struct pqg_chunk_result {
@@ -215,7 +217,9 @@ int pqg_bench_decode(pqg_ctx* ctx, const pqg_chunk_job* jobs, int n_jobs, int it
 /* Diagnostics of the last decode for job `job` (after pqg_sync): out[0] = 1
  * when its page list came from the serial header walk (K1e) instead of the
  * speculative parallel scan, out[1] = header candidates found, out[2] =
- * pages, out[3] = decompressed scratch bytes.  Returns entries written. */
+ * pages, out[3] = decompressed scratch bytes, out[4] = pipeline launches of
+ * the whole last decode call (1 unless an arena had to grow; grown capacities
+ * are remembered per chunk for later calls).  Returns entries written. */
 int pqg_debug_job(pqg_ctx* ctx, int job, int64_t* out, int cap);
 
 /* Diagnostic builds only (compiled with -DPQG_PROFILE): in-kernel phase cycle

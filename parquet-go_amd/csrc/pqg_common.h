@@ -70,6 +70,10 @@ struct PageDev {
   int32_t dict_width;      // RLE_DICTIONARY: index bit width byte
   int32_t hs_rep, hs_def, hs_val;  // hybrid streams of the page (HStream index, -1: none)
   int32_t pad;
+  // variable-length values (BYTE_ARRAY, FLBA of length 0): chars of the page
+  // and their offset in the chunk's chars (exclusive scan over the pages)
+  int64_t chars;
+  int64_t char_offset;
 };
 
 // One RLE/bit-packed hybrid stream (hybrid_decoder.go): a page's rep or def
@@ -135,8 +139,10 @@ struct JobDev {
   int64_t need_scratch;    // Σ usize of compressed blocks
   const uint8_t* dict_data;  // dictionary entries (fixed width) or chars (var)
   int64_t dict_count, dict_len;
-  const int64_t* dict_offs;  // variable-length dictionary offsets (count+1)
-  int32_t flags, pad;
+  const int64_t* dict_offs;  // variable-length dictionary: record start of each entry (count+1)
+  int32_t flags, pad;        // flags: bit0 INT96 nil entry (Q8), bit1 variable-length dictionary to walk
+  int64_t doffs_cap, doffs_base;  // dictionary-offsets arena region (entries)
+  int64_t need_doffs;             // entries the dictionary needs (count+1)
   // ---- K1 speculative page scan (see k_page_cands / k_page_chain)
   int64_t tile_base;       // first scan tile of this job (global tile index)
   int32_t n_tiles;         // ceil(min(tcs, data_len) / kScanTile)

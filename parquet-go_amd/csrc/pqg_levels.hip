@@ -154,8 +154,8 @@ __global__ void __launch_bounds__(256) k_page_setup(JobDev* jobs, PageDev* pages
       if (n > 0) reg_stream(job, streams, &pg.hs_val, pidx, 3, val + 4, take, 1, n);
     }
     // value-stage page lists: 4-byte dictionary pages (the hot path, a kernel
-    // of its own) and everything else
-    const int mode = (pg.encoding == 8 && job.value_width == 4) ? 1 : 0;
+    // of its own), variable-length values (pqg_strings.hip) and everything else
+    const int mode = job.value_width == 0 ? 2 : (pg.encoding == 8 && job.value_width == 4) ? 1 : 0;
     vlists[mode * list_cap + atomicAdd(&vcount[mode], 1)] = pidx;
   }
 }
@@ -476,6 +476,9 @@ __global__ void __launch_bounds__(256) k_nn_scan(JobDev* jobs, PageDev* pages, u
     if (job.value_width > 0 && vb > job.value_cap) job.status = kCAPACITY;
     job.values_bytes = vb;
     // dictionary page (page_dict.go:30-64): PLAIN entries of the column type.
+    // The dictionary is published only when the page's read phase succeeds:
+    // the gather sinks bound keys by dict_count alone, so a short page must
+    // never be visible (the reference fails the chunk in readPages first).
     if (job.dict_page >= 0 && job.dict_page < np) {
       PageDev& dp = pages[job.page_base + job.dict_page];
       if (dp.read_status == kOK) {
@@ -486,19 +489,30 @@ __global__ void __launch_bounds__(256) k_nn_scan(JobDev* jobs, PageDev* pages, u
         const int w = job.value_width;
         dp.block = blk;
         dp.block_len = blen;
+        int st = kOK;
+        int flags = 0;
         if (w > 0) {
           if (job.type == 3) {  // INT96: a partial final entry is left nil, not an error (Q8)
             const int64_t full = blen / 12, rem = blen % 12;
-            if (cnt > full + (rem > 0 ? 1 : 0)) dp.read_status = kEOF;
-            else if (cnt == full + 1 && rem > 0) job.flags |= 1;
+            if (cnt > full + (rem > 0 ? 1 : 0)) st = kEOF;
+            else if (cnt == full + 1 && rem > 0) flags = 1;
           } else if (cnt * w > blen) {
-            dp.read_status = kEOF;
+            st = kEOF;
           }
+        } else {
+          // u32-length entries (type_bytearray.go:24-45): k_str_dict walks them
+          // (every entry takes >= 4 bytes: a walk fails before entry blen/4 + 1)
+          flags = 2;
+          job.need_doffs = (cnt < blen / 4 ? cnt : blen / 4) + 2;
+          if (job.need_doffs > job.doffs_cap) job.status = kCAPACITY;
+        }
+        if (st == kOK) {
+          job.flags |= flags;
           job.dict_data = blk;
-          job.dict_count = cnt;
+          job.dict_count = (flags & 2) ? 0 : cnt;  // byte arrays: published by k_str_dict after its walk
           job.dict_len = blen;
         } else {
-          dp.read_status = kUNSUPPORTED;  // variable-length dictionaries: not in this build yet
+          dp.read_status = st;
         }
       }
     }

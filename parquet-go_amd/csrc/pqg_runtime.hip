@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <map>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -48,6 +49,13 @@ template <int Mode>
 __global__ void k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                          uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks);
 __global__ void k_finalize(JobDev* jobs, int n_jobs, PageDev* pages);
+__global__ void k_str_dict(JobDev* jobs, PageDev* pages, int64_t* doffs_arena);
+__global__ void k_str_count(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                            int64_t* offs_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks);
+__global__ void k_char_scan(JobDev* jobs, PageDev* pages, int64_t* offs_arena);
+__global__ void k_str_write(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                            uint8_t* value_arena, int64_t* offs_arena, const HStream* streams, const RunEnt* runs,
+                            const BlockDesc* blks);
 }  // namespace pqg
 
 #ifdef PQG_PROFILE
@@ -85,8 +93,24 @@ struct DevBuf {
   }
 };
 
-constexpr int kStages = 9;
-// stages timed by pqg_last_timings: scan (K1a-e), list, snappy, setup, walk, levels, nn_scan, values, finalize
+constexpr int kStages = 10;
+// stages timed by pqg_last_timings: scan (K1a-e), list, snappy, setup, walk, levels, nn_scan, values, strings,
+// finalize
+constexpr int kMaxAttempts = 6;  // decode + up to 5 arena grows in one pqg_sync
+
+// Arena capacities of one chunk job (see plan_batch); 0 = use the planner's estimate.
+struct Caps {
+  int64_t pages = 0, slots = 0, scratch = 0, values = 0, runs = 0, blks = 0, doffs = 0;
+};
+// Capacities learned for a chunk (its bytes, size and value count), kept for
+// later decodes of the same chunk so a grown arena is planned right away.
+struct JobKey {
+  uintptr_t data;
+  int64_t tcs, hint;
+  bool operator<(const JobKey& o) const {
+    return data != o.data ? data < o.data : tcs != o.tcs ? tcs < o.tcs : hint < o.hint;
+  }
+};
 
 int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
@@ -112,12 +136,16 @@ struct pqg_ctx {
   DevBuf streams, runs, blks;  // K3 hybrid run tables
   DevBuf cand_list, vlists;
   DevBuf asm_seg;  // K8 per-segment counts + totals
+  DevBuf offs_arena, doffs_arena;  // K7: value offsets (int64), dictionary record starts
   int64_t total_tiles = 0;
   JobDev* h_jobs = nullptr;  // pinned
   int h_jobs_cap = 0;
   std::vector<pqg_chunk_job> cur;       // jobs of the in-flight batch
   std::vector<JobDev> plan;             // per-job capacities used
-  std::vector<int64_t> force_pages, force_slots, force_scratch, force_values, force_runs, force_blks;
+  std::vector<Caps> force;              // per-job capacities forced for this batch
+  std::map<JobKey, Caps> learned;       // grown capacities, across calls
+  int launches = 0;                     // pipeline launches of the last decode
+  bool any_var = false;                 // batch holds variable-length columns
   int n_jobs = 0;
   int64_t list_cap = 0;
   hipEvent_t ev[kStages + 1];
@@ -179,7 +207,7 @@ void pqg_ctx_destroy(pqg_ctx* c) {
   for (auto& e : c->ev) hipEventDestroy(e);
   for (DevBuf* b : {&c->jobs, &c->pages, &c->list, &c->counters, &c->def_arena, &c->rep_arena, &c->value_arena,
                     &c->scratch, &c->streams, &c->runs, &c->blks, &c->cand_list, &c->vlists, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
-                    &c->ok2slot, &c->order, &c->asm_seg})
+                    &c->ok2slot, &c->order, &c->asm_seg, &c->offs_arena, &c->doffs_arena})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
   hipStreamDestroy(c->stream);
@@ -220,10 +248,11 @@ static int plan_batch(pqg_ctx* c) {
     if (hipHostMalloc((void**)&c->h_jobs, sizeof(JobDev) * (size_t)c->h_jobs_cap) != hipSuccess) return PQG_ERR_HIP;
   }
   int64_t page_total = 0, slot_total = 0, value_total = 0, scratch_total = 0, tile_total = 0, run_total = 0,
-          blk_total = 0;
+          blk_total = 0, offs_total = 0, doffs_total = 0;
   c->plan.resize((size_t)n);
   for (int i = 0; i < n; i++) {
     const pqg_chunk_job& in = c->cur[(size_t)i];
+    const Caps& f = c->force[(size_t)i];
     JobDev d;
     memset(&d, 0, sizeof(d));
     d.data = in.data;
@@ -238,25 +267,28 @@ static int plan_batch(pqg_ctx* c) {
     d.has_dict_off = in.has_dict_page_offset;
     d.value_width = value_width_of(in.col);
     int64_t pcap = in.total_compressed_size / 256 + 16;
-    if (c->force_pages[(size_t)i] > 0) pcap = c->force_pages[(size_t)i];
+    if (f.pages > 0) pcap = f.pages;
     pcap = std::min<int64_t>(pcap, (int64_t)1 << 30);
     d.page_cap = (int32_t)pcap;
     d.page_base = page_total;
     page_total += pcap;
     int64_t scap = std::max<int64_t>(in.num_values_hint, 0) + 64;
-    if (c->force_slots[(size_t)i] > 0) scap = c->force_slots[(size_t)i];
+    if (f.slots > 0) scap = f.slots;
     d.slot_cap = scap;
     d.slot_base = slot_total;
     slot_total += align_up(scap, 256);
-    int64_t vcap = d.value_width > 0 ? scap * d.value_width : 0;
-    if (c->force_values[(size_t)i] > 0) vcap = c->force_values[(size_t)i];
+    // variable-length values: chars estimated from the page bytes (dictionary
+    // chunks may need more: the first decode reports it and the arena grows)
+    int64_t vcap = d.value_width > 0 ? scap * d.value_width
+                                     : std::max<int64_t>(in.total_uncompressed_size, in.total_compressed_size) + 1024;
+    if (f.values > 0) vcap = f.values;
     d.value_cap = vcap;
     d.value_base = value_total;
     value_total += align_up(vcap, 256);
     int64_t xcap = 0;
     if (in.col.codec != PQG_CODEC_UNCOMPRESSED)
       xcap = std::max<int64_t>(in.total_uncompressed_size, in.total_compressed_size) + pcap * 16 + 1024;
-    if (c->force_scratch[(size_t)i] > 0) xcap = c->force_scratch[(size_t)i];
+    if (f.scratch > 0) xcap = f.scratch;
     d.scratch_cap = xcap;
     d.scratch_base = scratch_total;
     scratch_total += align_up(xcap, 256);
@@ -266,15 +298,26 @@ static int plan_batch(pqg_ctx* c) {
     // hybrid run tables: a stream of n bytes has at most n/2 + 2 runs, and a
     // page at most three streams (see reg_stream)
     int64_t rcap = (in.total_compressed_size + xcap) / 2 + 6 * pcap + 64;
-    if (c->force_runs[(size_t)i] > 0) rcap = c->force_runs[(size_t)i];
+    if (f.runs > 0) rcap = f.runs;
     d.run_cap = rcap;
     d.run_base = run_total;
     run_total += rcap;
     int64_t bcap = 3 * (scap / kHBlock + 3 * pcap) + rcap / kHBlockRuns + 2 * rcap / (kHBlockBytes / 2) + 64;
-    if (c->force_blks[(size_t)i] > 0) bcap = c->force_blks[(size_t)i];
+    if (f.blks > 0) bcap = f.blks;
     d.blk_cap = bcap;
     d.blk_base = blk_total;
     blk_total += bcap;
+    if (d.value_width == 0) {
+      d.offs_cap = scap + 1;
+      d.offs_base = offs_total;
+      offs_total += align_up(scap + 1, 32);
+      // dictionary entries take >= 4 bytes each
+      int64_t dcap = std::min<int64_t>(std::max<int64_t>(in.total_uncompressed_size, 0) / 4, 1 << 17) + 64;
+      if (f.doffs > 0) dcap = f.doffs;
+      d.doffs_cap = dcap;
+      d.doffs_base = doffs_total;
+      doffs_total += align_up(dcap, 32);
+    }
     d.tile_base = tile_total;
     d.n_tiles = (int32_t)((lim + kScanTile - 1) / kScanTile);
     tile_total += d.n_tiles;
@@ -291,13 +334,15 @@ static int plan_batch(pqg_ctx* c) {
       c->ok2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->cand_pos.grow(sizeof(int64_t) * (size_t)tile_total * kCandPerTile + 64) ||
       c->cand_list.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
-      c->vlists.grow(sizeof(int) * 2 * (size_t)page_total + 64) ||
+      c->vlists.grow(sizeof(int) * 3 * (size_t)page_total + 64) ||
       c->cands.grow(sizeof(Cand) * (size_t)tile_total * kCandPerTile + 64) ||
       c->succ.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->idx2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->order.grow(sizeof(int) * (size_t)page_total + 64) ||
       c->streams.grow(sizeof(HStream) * 3 * (size_t)page_total + 64) || c->runs.grow(sizeof(RunEnt) * (size_t)run_total + 64) ||
-      c->blks.grow(sizeof(BlockDesc) * (size_t)blk_total + 64))
+      c->blks.grow(sizeof(BlockDesc) * (size_t)blk_total + 64) ||
+      c->offs_arena.grow(sizeof(int64_t) * (size_t)offs_total + 64) ||
+      c->doffs_arena.grow(sizeof(int64_t) * (size_t)doffs_total + 64))
     return PQG_ERR_HIP;
   c->total_tiles = tile_total;
   return hip_ok(hipMemcpyAsync(c->jobs.p, c->h_jobs, sizeof(JobDev) * (size_t)n, hipMemcpyHostToDevice, c->stream));
@@ -305,6 +350,7 @@ static int plan_batch(pqg_ctx* c) {
 
 static int launch_pipeline(pqg_ctx* c) {
   const int n = c->n_jobs;
+  c->launches++;
   JobDev* jobs = (JobDev*)c->jobs.p;
   PageDev* pages = (PageDev*)c->pages.p;
   int* list = (int*)c->list.p;
@@ -370,8 +416,18 @@ static int launch_pipeline(pqg_ctx* c) {
   hipLaunchKernelGGL(k_values<0>, dim3(waves), dim3(64), 0, s, jobs, pages, vlists, ctr + 12, ctr + 10,
                      (uint8_t*)c->value_arena.p, streams, runs, blks);
   if (c->timed) hipEventRecord(c->ev[8], s);
-  hipLaunchKernelGGL(k_finalize, dim3(n), dim3(256), 0, s, jobs, n, pages);
+  if (c->any_var) {
+    int64_t* offs = (int64_t*)c->offs_arena.p;
+    hipLaunchKernelGGL(k_str_dict, dim3(n), dim3(64), 0, s, jobs, pages, (int64_t*)c->doffs_arena.p);
+    hipLaunchKernelGGL(k_str_count, dim3(waves), dim3(64), 0, s, jobs, pages, vlists + 2 * lcap, ctr + 14, ctr + 17,
+                       offs, streams, runs, blks);
+    hipLaunchKernelGGL(k_char_scan, dim3(n), dim3(256), 0, s, jobs, pages, offs);
+    hipLaunchKernelGGL(k_str_write, dim3(waves), dim3(64), 0, s, jobs, pages, vlists + 2 * lcap, ctr + 14, ctr + 18,
+                       (uint8_t*)c->value_arena.p, offs, streams, runs, blks);
+  }
   if (c->timed) hipEventRecord(c->ev[9], s);
+  hipLaunchKernelGGL(k_finalize, dim3(n), dim3(256), 0, s, jobs, n, pages);
+  if (c->timed) hipEventRecord(c->ev[10], s);
   return hip_ok(hipGetLastError());
 }
 
@@ -386,12 +442,14 @@ int pqg_decode_chunks_async(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs) {
   }
   c->cur.assign(jobs, jobs + n_jobs);
   c->n_jobs = n_jobs;
-  c->force_pages.assign((size_t)n_jobs, 0);
-  c->force_slots.assign((size_t)n_jobs, 0);
-  c->force_scratch.assign((size_t)n_jobs, 0);
-  c->force_values.assign((size_t)n_jobs, 0);
-  c->force_runs.assign((size_t)n_jobs, 0);
-  c->force_blks.assign((size_t)n_jobs, 0);
+  c->launches = 0;
+  c->force.assign((size_t)n_jobs, Caps());
+  c->any_var = false;
+  for (int i = 0; i < n_jobs; i++) {
+    auto it = c->learned.find(JobKey{(uintptr_t)jobs[i].data, jobs[i].total_compressed_size, jobs[i].num_values_hint});
+    if (it != c->learned.end()) c->force[(size_t)i] = it->second;
+    c->any_var |= value_width_of(jobs[i].col) == 0;
+  }
   if (n_jobs == 0) return PQG_OK;
   int e = plan_batch(c);
   if (e) return e;
@@ -404,7 +462,10 @@ int pqg_sync(pqg_ctx* c, pqg_chunk_result* results, int n_jobs) {
   hipSetDevice(c->device);
   const int n = c->n_jobs;
   if (n == 0) return PQG_OK;
-  for (int attempt = 0; attempt < 3; attempt++) {
+  // Every launch is followed by a copy-back and a sync, so the results below
+  // never describe a pipeline still in flight; a job still short of space
+  // after the last attempt reports PQG_ERR_CAPACITY.
+  for (int attempt = 0;; attempt++) {
     if (hipMemcpyAsync(c->h_jobs, c->jobs.p, sizeof(JobDev) * (size_t)n, hipMemcpyDeviceToHost, c->stream) !=
             hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
@@ -414,15 +475,23 @@ int pqg_sync(pqg_ctx* c, pqg_chunk_result* results, int n_jobs) {
       const JobDev& d = c->h_jobs[i];
       if (d.status != PQG_ERR_CAPACITY) continue;
       retry = true;
-      c->force_pages[(size_t)i] = std::max<int64_t>((int64_t)d.num_pages + 16, d.page_cap);
-      c->force_slots[(size_t)i] = std::max<int64_t>(d.num_slots + 64, d.slot_cap);
-      c->force_scratch[(size_t)i] = std::max<int64_t>(d.need_scratch + 1024, d.scratch_cap);
-      int64_t nv = std::max<int64_t>(d.num_values, d.num_slots);
-      c->force_values[(size_t)i] = std::max<int64_t>(nv * std::max(d.value_width, 1) + 64, d.value_cap);
-      c->force_runs[(size_t)i] = std::max<int64_t>(d.run_used + 64, d.run_cap);
-      c->force_blks[(size_t)i] = std::max<int64_t>(d.blk_used + 64, d.blk_cap);
+      Caps& f = c->force[(size_t)i];
+      f.pages = std::max<int64_t>((int64_t)d.num_pages + 16, d.page_cap);
+      f.slots = std::max<int64_t>(d.num_slots + 64, d.slot_cap);
+      f.scratch = std::max<int64_t>(d.need_scratch + 1024, d.scratch_cap);
+      if (d.value_width > 0) {
+        const int64_t nv = std::max<int64_t>(d.num_values, d.num_slots);
+        f.values = std::max<int64_t>(nv * d.value_width + 64, d.value_cap);
+      } else {
+        f.values = std::max<int64_t>(d.values_bytes + 1024, d.value_cap);
+      }
+      f.runs = std::max<int64_t>(d.run_used + 64, d.run_cap);
+      f.blks = std::max<int64_t>(d.blk_used + 64, d.blk_cap);
+      f.doffs = std::max<int64_t>(d.need_doffs + 64, d.doffs_cap);
+      const pqg_chunk_job& in = c->cur[(size_t)i];
+      c->learned[JobKey{(uintptr_t)in.data, in.total_compressed_size, in.num_values_hint}] = f;
     }
-    if (!retry) break;
+    if (!retry || attempt + 1 >= kMaxAttempts) break;
     int e = plan_batch(c);
     if (e) return e;
     e = launch_pipeline(c);
@@ -442,7 +511,7 @@ int pqg_sync(pqg_ctx* c, pqg_chunk_result* results, int n_jobs) {
     r.def_levels = d.max_def > 0 ? (uint8_t*)c->def_arena.p + d.slot_base : nullptr;
     r.rep_levels = d.max_rep > 0 ? (uint8_t*)c->rep_arena.p + d.slot_base : nullptr;
     r.values = (uint8_t*)c->value_arena.p + d.value_base;
-    r.offsets = nullptr;
+    r.offsets = d.value_width == 0 ? (int64_t*)c->offs_arena.p + d.offs_base : nullptr;
   }
   return PQG_OK;
 }
@@ -532,9 +601,9 @@ int pqg_debug_counters(pqg_ctx* c, uint64_t* out, int cap) {
 int pqg_debug_job(pqg_ctx* c, int job, int64_t* out, int cap) {
   if (!c || !out || job < 0 || job >= c->n_jobs) return PQG_ERR_INVALID_ARG;
   const JobDev& d = c->h_jobs[job];
-  const int64_t v[4] = {d.scan_fallback, d.n_cands, d.num_pages, d.need_scratch};
+  const int64_t v[5] = {d.scan_fallback, d.n_cands, d.num_pages, d.need_scratch, c->launches};
   int k = 0;
-  for (; k < 4 && k < cap; k++) out[k] = v[k];
+  for (; k < 5 && k < cap; k++) out[k] = v[k];
   return k;
 }
 
@@ -560,23 +629,18 @@ int pqg_bench_decode(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs, int iter
   // first call sizes the arenas (and retries on capacity)
   int e = pqg_decode_chunks(c, jobs, n_jobs, res.data());
   if (e) return e;
-  // freeze the capacities found by the first call
-  std::vector<int64_t> fp(c->force_pages), fs(c->force_slots), fx(c->force_scratch), fv(c->force_values),
-      fr(c->force_runs), fb(c->force_blks);
+  // the first call grew the arenas; its capacities are the learned ones now
   for (int i = 0; i < n_jobs; i++) {
-    fp[(size_t)i] = c->h_jobs[i].page_cap;
-    fs[(size_t)i] = c->h_jobs[i].slot_cap;
-    fx[(size_t)i] = c->h_jobs[i].scratch_cap;
-    fv[(size_t)i] = c->h_jobs[i].value_cap;
-    fr[(size_t)i] = c->h_jobs[i].run_cap;
-    fb[(size_t)i] = c->h_jobs[i].blk_cap;
+    Caps& f = c->force[(size_t)i];
+    const JobDev& d = c->h_jobs[i];
+    f.pages = d.page_cap;
+    f.slots = d.slot_cap;
+    f.scratch = d.scratch_cap;
+    f.values = d.value_cap;
+    f.runs = d.run_cap;
+    f.blks = d.blk_cap;
+    f.doffs = d.doffs_cap;
   }
-  c->force_runs = fr;
-  c->force_blks = fb;
-  c->force_pages = fp;
-  c->force_slots = fs;
-  c->force_scratch = fx;
-  c->force_values = fv;
   e = plan_batch(c);
   if (e) return e;
   hipEvent_t a, b;

@@ -131,6 +131,8 @@ __device__ __forceinline__ void init_page(PageDev& pg, int j, int64_t pos, int64
   pg.flags = 0;
   pg.dict_width = 0;
   pg.pad = 0;
+  pg.chars = 0;
+  pg.char_offset = 0;
 }
 
 __device__ __forceinline__ void init_job_results(JobDev& job) {
@@ -143,6 +145,7 @@ __device__ __forceinline__ void init_job_results(JobDev& job) {
   job.dict_count = 0;
   job.dict_len = 0;
   job.dict_offs = nullptr;
+  job.need_doffs = 0;
   job.status = kOK;
   job.error_page = -1;
   job.flags = 0;
@@ -703,7 +706,7 @@ __global__ void k_page_list(JobDev* jobs, int n_jobs, int* list, int list_cap, i
   }
   if (threadIdx.x == 0) {
     *total = off < list_cap ? off : list_cap;
-    for (int q = 0; q < 8; q++) queues[q] = 0;
+    for (int q = 0; q < 16; q++) queues[q] = 0;  // ctr[8..23]: queues and list counts
   }
 }
 

@@ -88,7 +88,7 @@ class DecodedColumn:
     """Decoded chunk on the host: def/rep levels + dense values[:nn] (readValues outputs)."""
 
     def __init__(self, status, error_page, num_slots, num_values, value_width, def_levels, rep_levels, values,
-                 pages):
+                 pages, offsets=None):
         self.status = status
         self.error_page = error_page
         self.num_slots = num_slots
@@ -96,7 +96,8 @@ class DecodedColumn:
         self.value_width = value_width
         self.def_levels = def_levels
         self.rep_levels = rep_levels
-        self.values = values
+        self.values = values          # fixed width: dense values; variable length: chars
+        self.offsets = offsets        # variable length: int64[num_values + 1]
         self.pages = pages
 
 
@@ -163,9 +164,9 @@ class GpuDecoder:
         return [buf[i] for i in range(k)]
 
     def debug_job(self, job_index):
-        """(serial_walk, candidates, pages, scratch_bytes) of the last decode."""
-        out = (C.c_int64 * 4)()
-        k = self.L.pqg_debug_job(self.ctx, job_index, out, 4)
+        """(serial_walk, candidates, pages, scratch_bytes, pipeline_launches) of the last decode."""
+        out = (C.c_int64 * 5)()
+        k = self.L.pqg_debug_job(self.ctx, job_index, out, 5)
         if k < 0:
             raise PqgError(k, "pqg_debug_job")
         return tuple(int(out[i]) for i in range(k))
@@ -201,9 +202,10 @@ class GpuDecoder:
         lv_def = self.d2h(r.def_levels, r.num_slots) if (r.def_levels and r.status == 0) else None
         lv_rep = self.d2h(r.rep_levels, r.num_slots) if (r.rep_levels and r.status == 0) else None
         vals = self.d2h(r.values, r.values_bytes) if r.status == 0 else None
+        offs = self.d2h(r.offsets, (r.num_values + 1) * 8, np.int64) if (r.offsets and r.status == 0) else None
         pages = self.pages(job_index) if job_index is not None else None
         return DecodedColumn(r.status, r.error_page, r.num_slots, r.num_values, r.value_width, lv_def, lv_rep,
-                             vals, pages)
+                             vals, pages, offs)
 
 
 def device_job(pf: ParquetFile, rg, col, dev_ptr_of_file):

@@ -24,6 +24,14 @@ def compare_chunk(exp, got, where=""):
         assert np.array_equal(got.def_levels, exp.def_levels), where + " def levels"
     if exp.rep_levels is not None:
         assert np.array_equal(got.rep_levels, exp.rep_levels), where + " rep levels"
+    if exp.value_width == 0:
+        # variable length: chars and int64 offsets[num_values + 1]
+        assert got.offsets is not None and exp.offsets is not None, where + " offsets missing"
+        assert np.array_equal(got.offsets, exp.offsets), where + " offsets"
+        assert got.values is not None and exp.values is not None
+        assert got.values.nbytes == exp.values.nbytes, "%s chars %d vs %d" % (where, got.values.nbytes,
+                                                                           exp.values.nbytes)
+        assert np.array_equal(got.values, exp.values), where + " chars"
     if exp.values is not None and exp.value_width > 0:
         assert got.values is not None
         assert got.values.nbytes == exp.values.nbytes, "%s values bytes %d vs %d" % (
