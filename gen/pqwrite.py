@@ -256,3 +256,104 @@ def config_c2_family(rows=100_000_000, bits_list=(1, 2, 4, 8, 12, 16, 20), null_
         col = Column("c2", INT32, vals, repetition=OPTIONAL, encoding=RLE_DICTIONARY, def_levels=defs,
                      rows_per_page=rows_per_page)
         yield bits, write_file([col], rows), (defs, vals)
+
+
+C5_ROWS_PER_RG = 15_625_000
+
+
+def _dbp_safe_rows_per_page(rows, rows_per_page):
+    """A page size whose pages all avoid the reference's DBP quirk Q3
+    (N == 1 or (N - 1) % 128 == 0 fails with EOF, deltabp_decoder.go:114-175)."""
+    bad = lambda n: n == 1 or (n - 1) % 128 == 0  # noqa: E731
+    rpp = rows_per_page
+    while bad(rpp) or (rows % rpp and bad(rows % rpp)):
+        rpp += 1
+    return rpp
+
+
+def c5_row_group_columns(rg, rows, seed=5, rows_per_page=20000):
+    """Column arrays of C5 row group `rg` (seeded by its global index, so any
+    subset of the 64 row groups can be generated independently):
+      lst   LIST<double> (3-level; length U{0..3}, 5% null lists, 5% null elements)
+      i32   int32 PLAIN          i64d  int64 DELTA_BINARY_PACKED
+      f64   double PLAIN         f32   float PLAIN
+      i96   int96 PLAIN          oi32  optional int32 RLE_DICTIONARY (10% nulls)
+      s     required string RLE_DICTIONARY (4096-word vocabulary, length U[4,32])
+      i64s  int64 PLAIN SNAPPY
+    Returns a dict name -> dict(values, def_levels, rep_levels, offsets)."""
+    rng = np.random.default_rng([seed, rg])
+    out = {}
+    # ---- LIST<double>
+    null_list = rng.random(rows) < 0.05
+    lens = rng.integers(0, 4, size=rows)
+    lens[null_list] = 0
+    per_row = np.where(lens == 0, 1, lens)
+    starts = np.zeros(rows + 1, np.int64)
+    starts[1:] = np.cumsum(per_row)
+    slots = int(starts[-1])
+    rep = np.ones(slots, np.uint8)
+    rep[starts[:-1]] = 0
+    row_of = np.repeat(np.arange(rows), per_row)
+    defs = np.full(slots, 3, np.uint8)
+    defs[rng.random(slots) < 0.05] = 2
+    empty = (lens == 0)[row_of]
+    defs[empty] = 1
+    defs[null_list[row_of]] = 0
+    nv = int((defs == 3).sum())
+    out["lst"] = dict(values=rng.standard_normal(nv), def_levels=defs, rep_levels=rep)
+    out["i32"] = dict(values=rng.integers(-2**31, 2**31 - 1, size=rows, dtype=np.int64).astype(np.int32))
+    steps = rng.integers(-1000, 1000, size=rows, dtype=np.int64)
+    out["i64d"] = dict(values=np.int64(rg) * 10**12 + np.cumsum(steps))
+    out["f64"] = dict(values=rng.standard_normal(rows))
+    out["f32"] = dict(values=rng.standard_normal(rows).astype(np.float32))
+    out["i96"] = dict(values=rng.integers(0, 256, size=rows * 12, dtype=np.uint8))
+    od = (rng.random(rows) >= 0.10).astype(np.uint8)
+    dvals = rng.integers(-2**31, 2**31 - 1, size=1000, dtype=np.int64).astype(np.int32)
+    out["oi32"] = dict(values=dvals[rng.integers(0, 1000, size=int(od.sum()))], def_levels=od)
+    chars, offs = make_vocab(4096, seed)
+    keys = rng.integers(0, 4096, size=rows)
+    lens_s = (offs[1:] - offs[:-1])[keys]
+    so = np.zeros(rows + 1, np.int64)
+    so[1:] = np.cumsum(lens_s)
+    idx = np.repeat(offs[:-1][keys] - so[:-1], lens_s) + np.arange(int(so[-1]), dtype=np.int64)
+    out["s"] = dict(values=chars[idx], offsets=so)
+    out["i64s"] = dict(values=rng.integers(-2**63, 2**63 - 1, size=rows, dtype=np.int64))
+    return out
+
+
+def config_c5(row_groups=(0,), rows_per_rg=C5_ROWS_PER_RG, seed=5, rows_per_page=20000):
+    """C5 row groups `row_groups` (global indices of the 64-row-group file; one
+    rank's shard under RG i -> GPU floor(i * G / 64)) written as one file, in
+    order.  Returns (file bytes, info)."""
+    parts = [c5_row_group_columns(rg, rows_per_rg, seed, rows_per_page) for rg in row_groups]
+
+    def cat(name, key):
+        arrs = [p[name].get(key) for p in parts]
+        if arrs[0] is None:
+            return None
+        if key == "offsets":
+            res, base = [np.zeros(1, np.int64)], 0
+            for a in arrs:
+                res.append(a[1:] + base)
+                base += int(a[-1])
+            return np.concatenate(res)
+        return np.concatenate(arrs)
+
+    rows = rows_per_rg * len(parts)
+    rpp_d = _dbp_safe_rows_per_page(rows_per_rg, rows_per_page)
+    cols = [
+        Column("lst", DOUBLE, cat("lst", "values"), repetition=LIST, def_levels=cat("lst", "def_levels"),
+               rep_levels=cat("lst", "rep_levels"), rows_per_page=rows_per_page),
+        Column("i32", INT32, cat("i32", "values"), rows_per_page=rows_per_page),
+        Column("i64d", INT64, cat("i64d", "values"), encoding=DELTA_BINARY_PACKED, rows_per_page=rpp_d),
+        Column("f64", DOUBLE, cat("f64", "values"), rows_per_page=rows_per_page),
+        Column("f32", FLOAT, cat("f32", "values"), rows_per_page=rows_per_page),
+        Column("i96", INT96, cat("i96", "values"), rows_per_page=rows_per_page),
+        Column("oi32", INT32, cat("oi32", "values"), repetition=OPTIONAL, encoding=RLE_DICTIONARY,
+               def_levels=cat("oi32", "def_levels"), rows_per_page=rows_per_page),
+        Column("s", BYTE_ARRAY, cat("s", "values"), offsets=cat("s", "offsets"), encoding=RLE_DICTIONARY,
+               rows_per_page=rows_per_page),
+        Column("i64s", INT64, cat("i64s", "values"), codec=SNAPPY, rows_per_page=rows_per_page),
+    ]
+    data = write_file(cols, rows, row_groups=len(parts))
+    return data, {"rows": rows, "row_groups": list(row_groups), "rows_per_rg": rows_per_rg}

@@ -257,6 +257,46 @@ typedef struct pqg_assemble_args {
 /* Enqueue K8 on the ctx stream and wait; fills the three counts. */
 int pqg_assemble(pqg_ctx* ctx, pqg_assemble_args* args);
 
+/* ---- K8 list export: Arrow LIST layout of a repeated leaf (max_rep == 1) ----
+ * The record assembly of a LIST column (Column.getData schema.go:235-264 over
+ * ColumnStore.get data_store.go:158-203) evaluated for every slot at once:
+ *   row start     rep[i] == 0 (rep_levels NULL: every slot)
+ *   element slot  def[i] >= elem_def          (the repeated group is present)
+ *   valid element def[i] == max_def           (consumes the next dense value)
+ *   row validity  def[row start] >= list_def  (else the list itself is null)
+ * For the 3-level LIST<T> written by parquet-mr / pyarrow (optional group (LIST)
+ * { repeated group list { optional T element } }: maxD = 3, maxR = 1):
+ * list_def = 1, elem_def = 2 — def 0 null list, 1 empty list, 2 null element,
+ * 3 value.  Outputs (DEVICE pointers, any may be NULL):
+ *   list_validity  one bit per row, LSB first           (zeroed by the call)
+ *   list_offsets   int32[rows + 1]: elements before each row, then the total
+ *   elem_validity  one bit per element, LSB first       (zeroed by the call)
+ *   elem_values    elements x value_width, null elements zeroed
+ * Buffers must hold rows / elements <= num_slots entries; the two bitmaps are
+ * written as whole dwords: give them 4 * ceil(num_slots / 32) bytes. */
+typedef struct pqg_list_args {
+  const uint8_t* def_levels; /* num_slots bytes (required)                        */
+  const uint8_t* rep_levels; /* num_slots bytes or NULL                           */
+  const uint8_t* values;     /* dense values (num_valid x value_width)            */
+  int64_t num_slots;
+  int32_t max_def;
+  int32_t list_def;
+  int32_t elem_def;
+  int32_t value_width;
+  uint8_t* list_validity;
+  int32_t* list_offsets;
+  uint8_t* elem_validity;
+  uint8_t* elem_values;
+  int64_t num_rows;          /* out */
+  int64_t num_elements;      /* out */
+  int64_t num_valid;         /* out: valid elements (= dense values consumed)     */
+  int64_t null_lists;        /* out */
+} pqg_list_args;
+
+/* Enqueue the list export on the ctx stream and wait; fills the counts.
+ * PQG_ERR_INVALID_ARG when elements exceed int32 offsets. */
+int pqg_assemble_list(pqg_ctx* ctx, pqg_list_args* args);
+
 /* ---- host-side planner: footer / schema (file_meta.go:14-62, schema.go) --- */
 typedef struct pqg_file pqg_file;
 
@@ -300,6 +340,9 @@ int pqo_hybrid_decode(const uint8_t* buf, int64_t len, int width, int64_t count,
 int pqo_snappy_decode(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int64_t* out_len);
 int pqo_delta_decode64(const uint8_t* buf, int64_t len, int64_t count, int64_t* out);
 int pqo_delta_decode32(const uint8_t* buf, int64_t len, int64_t count, int32_t* out);
+/* K8 restatements (host pointers): the ColumnStore.get / getData cursor walks */
+int pqo_assemble(pqg_assemble_args* args);
+int pqo_assemble_list(pqg_list_args* args);
 
 #ifdef __cplusplus
 }

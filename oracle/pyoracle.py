@@ -35,6 +35,7 @@ def lib():
         L.pqo_delta_decode64.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_void_p]
         L.pqo_delta_decode32.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_void_p]
         L.pqo_assemble.argtypes = [C.POINTER(abi.AssembleArgs)]
+        L.pqo_assemble_list.argtypes = [C.POINTER(abi.ListArgs)]
         _lib = L
     return _lib
 
@@ -128,3 +129,28 @@ def assemble(def_levels, rep_levels, values, max_def, boundary_level, value_widt
     assert rc == 0
     return (validity[:(n + 7) // 8], spaced[:n * value_width], offsets[:a.num_boundaries + 1],
             (a.num_valid, a.null_count, a.num_boundaries))
+
+
+def assemble_list(def_levels, rep_levels, values, max_def, list_def, elem_def, value_width):
+    """K8 list export oracle: returns (list_validity, list_offsets, elem_validity,
+    elem_values, (rows, elements, valid, null_lists)); bitmaps trimmed to their bits."""
+    n = len(def_levels)
+    d = np.ascontiguousarray(def_levels, dtype=np.uint8)
+    r = None if rep_levels is None else np.ascontiguousarray(rep_levels, dtype=np.uint8)
+    v = np.ascontiguousarray(values if values is not None else np.zeros(1, np.uint8)).view(np.uint8)
+    lv = np.zeros(max((n + 7) // 8, 1), np.uint8)
+    ev = np.zeros(max((n + 7) // 8, 1), np.uint8)
+    lo = np.zeros(n + 1, np.int32)
+    evals = np.zeros(max(n * value_width, 1), np.uint8)
+    a = abi.ListArgs()
+    a.def_levels = d.ctypes.data
+    a.rep_levels = r.ctypes.data if r is not None else None
+    a.values = v.ctypes.data
+    a.num_slots, a.max_def, a.list_def, a.elem_def, a.value_width = n, max_def, list_def, elem_def, value_width
+    a.list_validity, a.list_offsets, a.elem_validity = lv.ctypes.data, lo.ctypes.data, ev.ctypes.data
+    a.elem_values = evals.ctypes.data if value_width else None
+    rc = lib().pqo_assemble_list(C.byref(a))
+    assert rc == 0, rc
+    rows, el = a.num_rows, a.num_elements
+    return (lv[:(rows + 7) // 8], lo[:rows + 1], ev[:(el + 7) // 8], evals[:el * value_width],
+            (rows, el, a.num_valid, a.null_lists))

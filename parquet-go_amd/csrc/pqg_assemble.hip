@@ -164,6 +164,186 @@ __global__ void __launch_bounds__(256) k_asm_write(const uint8_t* def_, const ui
   }
 }
 
+// ---------------------------------------------------------------------------
+// List export (pqg_assemble_list): Arrow LIST layout of a repeated leaf.
+// Three predicates per slot — row start (rep == 0), element (def >= elem_def),
+// valid element (def == max_def) — give three ranks per slot, all popcounts of
+// ballots plus the segment bases from the scan.  Row and element validity bits
+// are not slot-aligned: the wave compresses each ballot's bits to rank order
+// with one ds_permute (lane l pushes its bit to lane rank(l)) and ORs the
+// packed word into the bitmap at the running bit offset.
+// ---------------------------------------------------------------------------
+struct ListPred {
+  bool row, elem, valid, list_ok;
+};
+__device__ __forceinline__ ListPred list_pred(const PQG_G uint8_t* def, const PQG_G uint8_t* rep, int64_t i, bool in,
+                                              int max_def, int list_def, int elem_def) {
+  ListPred p;
+  const int d = in ? (int)def[i] : -1;
+  p.row = in && (rep == nullptr || rep[i] == 0);
+  p.elem = in && d >= elem_def;
+  p.valid = in && d == max_def;
+  p.list_ok = p.row && d >= list_def;
+  return p;
+}
+
+__global__ void __launch_bounds__(256) k_list_count(const uint8_t* def_, const uint8_t* rep_, int64_t n, int max_def,
+                                                    int list_def, int elem_def, int64_t nseg, int64_t* seg_cnt) {
+  const PQG_G uint8_t* def = gconst(def_);
+  const PQG_G uint8_t* rep = gconst(rep_);
+  const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (seg >= nseg) return;
+  const int lane = lane64();
+  const int64_t s0 = seg * kAsmSeg, s1 = s0 + kAsmSeg < n ? s0 + kAsmSeg : n;
+  int64_t nr = 0, ne = 0, nv = 0, nl = 0;
+  for (int64_t b = s0; b < s1; b += 64) {
+    const ListPred p = list_pred(def, rep, b + lane, b + lane < s1, max_def, list_def, elem_def);
+    nr += __popcll(ballot64(p.row));
+    ne += __popcll(ballot64(p.elem));
+    nv += __popcll(ballot64(p.valid));
+    nl += __popcll(ballot64(p.row && !p.list_ok));
+  }
+  if (lane == 0) {
+    PQG_G int64_t* o = gmut(seg_cnt) + 4 * seg;
+    o[0] = nr;
+    o[1] = ne;
+    o[2] = nv;
+    o[3] = nl;
+  }
+}
+
+// Exclusive scan of the 4 per-segment counters in place; tot[0..3] = totals;
+// list_offsets[rows] = elements.
+__global__ void __launch_bounds__(1024) k_list_scan(int64_t* seg_cnt, int64_t nseg, int64_t* tot,
+                                                    int32_t* list_offsets) {
+  __shared__ int64_t sc[4][1024];
+  __shared__ int64_t carry[4];
+  const int t = threadIdx.x;
+  if (t < 4) carry[t] = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < nseg; base += 1024) {
+    const int64_t k = base + t;
+    int64_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      v[j] = k < nseg ? seg_cnt[4 * k + j] : 0;
+      sc[j][t] = v[j];
+    }
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+      int64_t a[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) a[j] = t >= d ? sc[j][t - d] : 0;
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 4; j++) sc[j][t] += a[j];
+      __syncthreads();
+    }
+    if (k < nseg) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) seg_cnt[4 * k + j] = carry[j] + sc[j][t] - v[j];
+    }
+    __syncthreads();
+    if (t < 4) carry[t] += sc[t][1023];
+    __syncthreads();
+  }
+  if (t == 0) {
+    for (int j = 0; j < 4; j++) tot[j] = carry[j];
+    if (list_offsets) list_offsets[carry[0]] = (int32_t)carry[1];
+  }
+}
+
+// bits of `m` (ballot order) packed to rank order under mask `sel`: bit k of
+// the result = m's bit at the k-th set lane of sel
+__device__ __forceinline__ uint64_t compress_ballot(bool bit, bool in_sel, uint64_t sel, uint64_t lt) {
+  const int rank = in_sel ? __popcll(sel & lt) : __popcll(sel) + __popcll(~sel & lt);
+  const int got = __builtin_amdgcn_ds_permute(rank << 2, (int)bit);
+  return ballot64(lane64() < __popcll(sel) && got != 0);
+}
+
+// OR packed bits into a bitmap at bit offset `at` (atomic: neighbouring
+// waves share the boundary words); the bits span at most three dwords
+__device__ __forceinline__ void or_bits(uint32_t* bm, int64_t at, uint64_t bits) {
+  if (bits == 0) return;
+  uint32_t* w = bm + (at >> 5);
+  const int sh = (int)(at & 31);
+  const uint32_t q0 = (uint32_t)(bits << sh);
+  const uint32_t q1 = (uint32_t)(bits >> (32 - sh));  // sh = 0: bits >> 32
+  const uint32_t q2 = sh ? (uint32_t)(bits >> (64 - sh)) : 0u;
+  if (q0) atomicOr(w, q0);
+  if (q1) atomicOr(w + 1, q1);
+  if (q2) atomicOr(w + 2, q2);
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) k_list_write(const uint8_t* def_, const uint8_t* rep_, const uint8_t* values_,
+                                                    int64_t n, int max_def, int list_def, int elem_def, int w,
+                                                    int64_t nseg, const int64_t* seg_cnt, uint8_t* list_validity_,
+                                                    int32_t* list_offsets_, uint8_t* elem_validity_,
+                                                    uint8_t* elem_values_) {
+  const PQG_G uint8_t* def = gconst(def_);
+  const PQG_G uint8_t* rep = gconst(rep_);
+  const PQG_G uint8_t* values = gconst(values_);
+  PQG_G int32_t* list_offsets = gmut(list_offsets_);
+  PQG_G uint8_t* elem_values = gmut(elem_values_);
+  uint32_t* lval = (uint32_t*)list_validity_;
+  uint32_t* evalid = (uint32_t*)elem_validity_;
+  const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (seg >= nseg) return;
+  const int lane = lane64();
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const int64_t s0 = seg * kAsmSeg, s1 = s0 + kAsmSeg < n ? s0 + kAsmSeg : n;
+  const PQG_G int64_t* sc = gconst(seg_cnt) + 4 * seg;
+  int64_t rb = sc[0], eb = sc[1], vb = sc[2];
+  for (int64_t b = s0; b < s1; b += 64) {
+    const int64_t i = b + lane;
+    const ListPred p = list_pred(def, rep, i, i < s1, max_def, list_def, elem_def);
+    const uint64_t mr = ballot64(p.row), me = ballot64(p.elem), mv = ballot64(p.valid);
+    const int64_t e = eb + __popcll(me & lt);
+    if (p.row && list_offsets) list_offsets[rb + __popcll(mr & lt)] = (int32_t)e;
+    if (p.elem && elem_values)
+      copy_value<W>(elem_values + e * w, values + (vb + __popcll(mv & lt)) * w, p.valid, w);
+    if (list_validity_) {
+      const uint64_t bits = compress_ballot(p.list_ok, p.row, mr, lt);
+      if (lane == 0) or_bits(lval, rb, bits);
+    }
+    if (elem_validity_) {
+      const uint64_t bits = compress_ballot(p.valid, p.elem, me, lt);
+      if (lane == 0) or_bits(evalid, eb, bits);
+    }
+    rb += __popcll(mr);
+    eb += __popcll(me);
+    vb += __popcll(mv);
+  }
+}
+
+int list_launch(hipStream_t s, const pqg_list_args* a, int64_t* seg_scratch, int64_t* tot) {
+  const int64_t n = a->num_slots;
+  const int64_t nseg = (n + kAsmSeg - 1) / kAsmSeg;
+  const unsigned blocks = (unsigned)((nseg + 3) / 4);
+  const int w = a->elem_values ? a->value_width : 0;
+  const size_t bm_bytes = (size_t)((n + 31) / 32) * 4;  // whole dwords (see pqgpu.h)
+  if (a->list_validity && bm_bytes) hipMemsetAsync(a->list_validity, 0, bm_bytes, s);
+  if (a->elem_validity && bm_bytes) hipMemsetAsync(a->elem_validity, 0, bm_bytes, s);
+  if (nseg > 0)
+    hipLaunchKernelGGL(k_list_count, dim3(blocks), dim3(256), 0, s, a->def_levels, a->rep_levels, n, a->max_def,
+                       a->list_def, a->elem_def, nseg, seg_scratch);
+  hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(1024), 0, s, seg_scratch, nseg, tot, a->list_offsets);
+  if (nseg == 0) return hipGetLastError() == hipSuccess ? PQG_OK : PQG_ERR_HIP;
+#define PQG_LST(WW)                                                                                                  \
+  hipLaunchKernelGGL(k_list_write<WW>, dim3(blocks), dim3(256), 0, s, a->def_levels, a->rep_levels, a->values, n,   \
+                     a->max_def, a->list_def, a->elem_def, w, nseg, (const int64_t*)seg_scratch, a->list_validity,  \
+                     a->list_offsets, a->elem_validity, a->elem_values)
+  switch (w) {
+    case 1: PQG_LST(1); break;
+    case 4: PQG_LST(4); break;
+    case 8: PQG_LST(8); break;
+    default: PQG_LST(0); break;
+  }
+#undef PQG_LST
+  return hipGetLastError() == hipSuccess ? PQG_OK : PQG_ERR_HIP;
+}
+
 // Host launcher (called from pqg_assemble in pqg_runtime.hip).  seg_scratch
 // holds 2 × nseg int64; tot 2 int64 (device).
 int assemble_launch(hipStream_t s, const pqg_assemble_args* a, int64_t* seg_scratch, int64_t* tot) {

@@ -20,6 +20,7 @@
 
 namespace pqg {
 int assemble_launch(hipStream_t s, const pqg_assemble_args* a, int64_t* seg_scratch, int64_t* tot);  // pqg_assemble.hip
+int list_launch(hipStream_t s, const pqg_list_args* a, int64_t* seg_scratch, int64_t* tot);          // pqg_assemble.hip
 }
 
 namespace pqg {
@@ -535,6 +536,28 @@ int pqg_assemble(pqg_ctx* c, pqg_assemble_args* a) {
   a->null_count = a->num_slots - h[0];
   a->num_boundaries = h[1];
   return PQG_OK;
+}
+
+int pqg_assemble_list(pqg_ctx* c, pqg_list_args* a) {
+  if (!c || !a || a->num_slots < 0 || !a->def_levels || a->max_def < 0 || a->max_def > 255 || a->value_width < 0)
+    return PQG_ERR_INVALID_ARG;
+  if (a->elem_values && (a->value_width <= 0 || (!a->values && a->num_slots > 0))) return PQG_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  const int64_t nseg = (a->num_slots + 4095) / 4096;
+  if (c->asm_seg.grow((size_t)(4 * nseg + 4) * sizeof(int64_t))) return PQG_ERR_HIP;
+  int64_t* seg = (int64_t*)c->asm_seg.p;
+  int64_t* tot = seg + 4 * nseg;
+  int e = pqg::list_launch(c->stream, a, seg, tot);
+  if (e) return e;
+  int64_t h[4] = {0, 0, 0, 0};
+  if (hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return PQG_ERR_HIP;
+  a->num_rows = h[0];
+  a->num_elements = h[1];
+  a->num_valid = h[2];
+  a->null_lists = h[3];
+  return h[1] > INT32_MAX ? PQG_ERR_INVALID_ARG : PQG_OK;
 }
 
 int pqg_decode_chunks(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs, pqg_chunk_result* results) {

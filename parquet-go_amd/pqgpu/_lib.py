@@ -39,6 +39,7 @@ def lib():
         "pqg_debug_counters": ([P, C.POINTER(C.c_uint64), I], I),
         "pqg_bench_decode": ([P, C.POINTER(abi.ChunkJob), I, I, C.POINTER(C.c_float), C.POINTER(C.c_float), I], I),
         "pqg_assemble": ([P, C.POINTER(abi.AssembleArgs)], I),
+        "pqg_assemble_list": ([P, C.POINTER(abi.ListArgs)], I),
         "pqg_file_open": ([C.c_char_p, I64, C.POINTER(P)], I),
         "pqg_file_close": ([P], None),
         "pqg_file_num_columns": ([P], I),
@@ -59,7 +60,8 @@ def lib():
 EXPORTED = [
     "pqg_ctx_create", "pqg_ctx_destroy", "pqg_status_string", "pqg_device_alloc", "pqg_device_free",
     "pqg_memcpy_h2d", "pqg_memcpy_d2h", "pqg_decode_chunks_async", "pqg_sync", "pqg_decode_chunks",
-    "pqg_get_pages", "pqg_last_timings", "pqg_debug_job", "pqg_debug_counters", "pqg_bench_decode", "pqg_assemble", "pqg_file_open", "pqg_file_close",
+    "pqg_get_pages", "pqg_last_timings", "pqg_debug_job", "pqg_debug_counters", "pqg_bench_decode", "pqg_assemble",
+    "pqg_assemble_list", "pqg_file_open", "pqg_file_close",
     "pqg_file_num_columns", "pqg_file_num_row_groups", "pqg_file_num_rows", "pqg_file_row_group_rows",
     "pqg_file_column", "pqg_file_chunk",
 ]

@@ -133,5 +133,16 @@ class AssembleArgs(C.Structure):
                 ("num_valid", C.c_int64), ("null_count", C.c_int64), ("num_boundaries", C.c_int64)]
 
 
+class ListArgs(C.Structure):
+    """pqg_list_args (include/pqgpu.h, K8 list export)."""
+    _fields_ = [("def_levels", C.c_void_p), ("rep_levels", C.c_void_p), ("values", C.c_void_p),
+                ("num_slots", C.c_int64), ("max_def", C.c_int32), ("list_def", C.c_int32),
+                ("elem_def", C.c_int32), ("value_width", C.c_int32),
+                ("list_validity", C.c_void_p), ("list_offsets", C.c_void_p), ("elem_validity", C.c_void_p),
+                ("elem_values", C.c_void_p),
+                ("num_rows", C.c_int64), ("num_elements", C.c_int64), ("num_valid", C.c_int64),
+                ("null_lists", C.c_int64)]
+
+
 def status_name(code):
     return STATUS.get(int(code), str(code))

@@ -198,6 +198,28 @@ class GpuDecoder:
         _check(self.L.pqg_assemble(self.ctx, C.byref(a)), "pqg_assemble")
         return a, vp, sp, op
 
+    def assemble_list(self, def_ptr, rep_ptr, values_ptr, num_slots, max_def, list_def=1, elem_def=2,
+                      value_width=0, values=True):
+        """K8 list export (Arrow LIST layout) of device level/value arrays.
+        Returns (ListArgs, list_validity, list_offsets, elem_validity, elem_values)
+        device pointers (elem_values None unless `values`)."""
+        a = abi.ListArgs()
+        a.def_levels, a.rep_levels, a.values = def_ptr, rep_ptr or None, values_ptr or None
+        a.num_slots, a.max_def, a.list_def, a.elem_def = num_slots, max_def, list_def, elem_def
+        a.value_width = value_width
+
+        def alloc(nbytes):
+            p = C.c_void_p()
+            _check(self.L.pqg_device_alloc(self.ctx, max(nbytes, 1), C.byref(p)), "pqg_device_alloc")
+            self._bufs.append(p)
+            return p.value
+
+        bm = (num_slots + 31) // 32 * 4
+        a.list_validity, a.list_offsets, a.elem_validity = alloc(bm), alloc((num_slots + 1) * 4), alloc(bm)
+        a.elem_values = alloc(num_slots * value_width) if values and value_width else None
+        _check(self.L.pqg_assemble_list(self.ctx, C.byref(a)), "pqg_assemble_list")
+        return a, a.list_validity, a.list_offsets, a.elem_validity, a.elem_values
+
     def download(self, r, job_index=None):
         lv_def = self.d2h(r.def_levels, r.num_slots) if (r.def_levels and r.status == 0) else None
         lv_rep = self.d2h(r.rep_levels, r.num_slots) if (r.rep_levels and r.status == 0) else None

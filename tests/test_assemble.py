@@ -189,3 +189,130 @@ def test_gpu_assemble_multi_pass_scan(dec):
     defs, reps, vals = _random_case(rng, n, 3, True, 4)
     exp = O.assemble(defs, reps, vals, 3, 0, 4)
     _check(_gpu_assemble(dec, defs, reps, vals, 3, 0, 4), exp)
+
+
+# ---------------------------------------------------------------- K8 list export (Arrow LIST)
+
+def _c5_list_chunk(rows=40_000, rg=0):
+    import pqgpu
+    import parity as P
+    from gen import pqwrite as W
+    data, _ = W.config_c5(row_groups=(rg,), rows_per_rg=rows)
+    pf = pqgpu.ParquetFile(data)
+    return data, pf, P.oracle_chunk(pf, 0, 0)
+
+
+def test_oracle_list_export_matches_pyarrow():
+    """pqo_assemble_list on the oracle's decode of C5's LIST<double> chunk equals
+    pyarrow's ListArray (an independent reader): offsets, list validity, element
+    validity and element values."""
+    import io
+    import pyarrow.parquet as pq
+    data, pf, ch = _c5_list_chunk()
+    lv, lo, ev, evals, cnt = O.assemble_list(ch.def_levels, ch.rep_levels, ch.values, 3, 1, 2, 8)
+    arr = pq.read_table(io.BytesIO(data)).column("lst").combine_chunks()
+    rows = len(arr)
+    assert cnt[0] == rows and cnt[3] == arr.null_count
+    assert np.array_equal(lo, np.asarray(arr.offsets))
+    assert np.array_equal(np.unpackbits(lv, bitorder="little")[:rows].astype(bool), np.asarray(arr.is_valid()))
+    flat = arr.values
+    assert cnt[1] == len(flat) and cnt[2] == len(flat) - flat.null_count
+    assert np.array_equal(np.unpackbits(ev, bitorder="little")[:cnt[1]].astype(bool), np.asarray(flat.is_valid()))
+    got = evals.view(np.float64)
+    exp = np.asarray(flat.fill_null(0.0))
+    assert np.array_equal(got.view(np.uint64), exp.view(np.uint64))
+
+
+def _random_lists(rng, rows, null_list=0.05, null_elem=0.05, max_len=4):
+    lens = rng.integers(0, max_len, size=rows)
+    nl = rng.random(rows) < null_list
+    per = np.where((lens == 0) | nl, 1, lens)
+    st = np.r_[0, np.cumsum(per)]
+    rep = np.ones(int(st[-1]), np.uint8)
+    rep[st[:-1]] = 0
+    row_of = np.repeat(np.arange(rows), per)
+    defs = np.where(rng.random(len(rep)) < null_elem, 2, 3).astype(np.uint8)
+    defs[((lens == 0) & ~nl)[row_of]] = 1
+    defs[nl[row_of]] = 0
+    vals = rng.standard_normal(int((defs == 3).sum()))
+    return defs, rep, vals
+
+
+def test_oracle_list_closed_form():
+    rng = np.random.default_rng(3)
+    defs, rep, vals = _random_lists(rng, 5000)
+    lv, lo, ev, evals, cnt = O.assemble_list(defs, rep, vals, 3, 1, 2, 8)
+    starts = np.flatnonzero(rep == 0)
+    el = defs >= 2
+    assert np.array_equal(lo, np.r_[np.cumsum(el)[starts] - el[starts], el.sum()].astype(np.int32))
+    assert np.array_equal(np.unpackbits(lv, bitorder="little")[:len(starts)].astype(bool), defs[starts] >= 1)
+    ev_exp = defs[el] == 3
+    assert np.array_equal(np.unpackbits(ev, bitorder="little")[:cnt[1]].astype(bool), ev_exp)
+    spaced = np.zeros(cnt[1])
+    spaced[ev_exp] = vals
+    assert np.array_equal(evals.view(np.float64), spaced)
+
+
+def _gpu_list(dec, defs, reps, vals, w):
+    n = len(defs)
+    dp = dec.upload(np.ascontiguousarray(defs, np.uint8))
+    rp = dec.upload(np.ascontiguousarray(reps, np.uint8)) if reps is not None else None
+    vp = dec.upload(np.ascontiguousarray(vals).view(np.uint8)) if w and len(vals) else (dec.upload(b"\0") if w else None)
+    a, lvp, lop, evp, vvp = dec.assemble_list(dp, rp, vp, n, 3, 1, 2, w, values=w > 0)
+    rows, el = a.num_rows, a.num_elements
+    got = (dec.d2h(lvp, (rows + 7) // 8), dec.d2h(lop, (rows + 1) * 4, np.int32), dec.d2h(evp, (el + 7) // 8),
+           dec.d2h(vvp, el * w) if w else np.zeros(0, np.uint8), (a.num_rows, a.num_elements, a.num_valid, a.null_lists))
+    for p in (dp, rp, vp, lvp, lop, evp, vvp):
+        if p:
+            dec.free(p)
+    return got
+
+
+def _check_list(got, exp):
+    for k, name in enumerate(("list validity", "list offsets", "element validity", "element values")):
+        assert np.array_equal(got[k], exp[k]), name
+    assert tuple(got[4]) == tuple(exp[4]), "counts"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [0, 1, 40, 2000, 3001, 250_000, 3_000_000])
+def test_gpu_list_export_random(dec, rows):
+    rng = np.random.default_rng(rows + 1)
+    defs, rep, vals = _random_lists(rng, rows, null_list=0.1, null_elem=0.2)
+    exp = O.assemble_list(defs, rep, vals, 3, 1, 2, 8)
+    _check_list(_gpu_list(dec, defs, rep, vals, 8), exp)
+
+
+@pytest.mark.gpu
+def test_gpu_list_export_malformed_levels(dec):
+    """Unvalidated levels (Q6): leading rep > 0 slots, rep > 0 with def < elem_def."""
+    rng = np.random.default_rng(9)
+    n = 20_000
+    defs = rng.integers(0, 4, size=n).astype(np.uint8)
+    rep = rng.integers(0, 2, size=n).astype(np.uint8)
+    rep[:5] = 1
+    vals = rng.standard_normal(int((defs == 3).sum()))
+    exp = O.assemble_list(defs, rep, vals, 3, 1, 2, 8)
+    _check_list(_gpu_list(dec, defs, rep, vals, 8), exp)
+
+
+@pytest.mark.gpu
+def test_gpu_list_export_decoded_c5(dec):
+    """Decode C5's LIST<double> chunk on the GPU, export it on the GPU, and match
+    the oracle's decode + export (itself pinned to pyarrow above)."""
+    import pqgpu
+    data, pf, ch = _c5_list_chunk(rows=60_000, rg=7)
+    devp = dec.upload(pf.data)
+    try:
+        r = dec.decode_jobs([pqgpu.device_job(pf, 0, 0, devp)])[0]
+        assert r.status == 0
+        a, lvp, lop, evp, vvp = dec.assemble_list(r.def_levels, r.rep_levels, r.values, r.num_slots, 3, 1, 2, 8)
+        rows, el = a.num_rows, a.num_elements
+        got = (dec.d2h(lvp, (rows + 7) // 8), dec.d2h(lop, (rows + 1) * 4, np.int32), dec.d2h(evp, (el + 7) // 8),
+               dec.d2h(vvp, el * 8), (a.num_rows, a.num_elements, a.num_valid, a.null_lists))
+        _check_list(got, O.assemble_list(ch.def_levels, ch.rep_levels, ch.values, 3, 1, 2, 8))
+        assert rows == 60_000 and a.num_valid == r.num_values
+        for p in (lvp, lop, evp, vvp):
+            dec.free(p)
+    finally:
+        dec.free(devp)

@@ -507,3 +507,18 @@ def test_capacity_grows_once_then_remembered(dec):
         assert first >= 3 and second == 1, (first, second)
     finally:
         dec.free(dev)
+
+
+# ---------------------------------------------------------------- C5: nested list + 8 mixed columns
+def test_c5_every_column(dec):
+    """Reduced-row C5 (LIST<double> + 8 mixed columns, 3 row groups): every
+    chunk of every row group against the oracle."""
+    data, _ = W.config_c5(row_groups=(0, 31, 63), rows_per_rg=45_000)
+    res = P.compare_file(data, dec)
+    assert len(res) == 27 and all(r.status == 0 for r in res)
+
+
+def test_c5_single_page_chunks(dec):
+    """parquet-go's own writer puts one data page in each chunk (chunk_writer.go:237-246)."""
+    data, _ = W.config_c5(row_groups=(5,), rows_per_rg=30_000, rows_per_page=30_000)
+    P.compare_file(data, dec)

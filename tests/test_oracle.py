@@ -277,3 +277,34 @@ def test_crash_files_never_crash():
                 except pqgpu.PqgError:
                     continue
                 O.decode_chunk(job)  # any status is fine; must not crash
+
+
+def test_c5_columns_against_arrow():
+    """C5 (two row groups): every flat column's oracle decode equals pyarrow's."""
+    import pyarrow as pa
+    data, _ = W.config_c5(row_groups=(2, 9), rows_per_rg=20_000)
+    pf, res = _decode_file(data)
+    assert all(r.status == 0 for (_, _, r) in res)
+    dt = {1: np.int32, 2: np.int64, 3: np.int64, 4: np.float32, 5: np.float64}
+    for c in range(1, pf.num_columns):
+        name = pf.columns[c].path.decode()
+        parts = [r for (_, cc, r) in res if cc == c]
+        arr = U.arrow_column(data, c).combine_chunks()
+        if name == "s":
+            got = []
+            for r in parts:
+                got += [r.values[r.offsets[i]:r.offsets[i + 1]].tobytes() for i in range(r.num_values)]
+            assert got == [x.as_py().encode() for x in arr]
+        elif name == "i96":
+            # pyarrow converts INT96 to timestamps; compare the raw 12-byte values with the generator's
+            rg_cols = [W.c5_row_group_columns(rg, 20_000)["i96"]["values"] for rg in (2, 9)]
+            assert np.array_equal(np.concatenate([r.values for r in parts]), np.concatenate(rg_cols))
+        else:
+            t = dt[pf.columns[c].desc.physical_type]
+            got = np.concatenate([r.values.view(t) for r in parts])
+            exp = U.dense_values(U.arrow_column(data, c), t)
+            assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), name
+            if name == "oi32":
+                defs = np.concatenate([r.def_levels for r in parts]).astype(bool)
+                assert np.array_equal(defs, np.asarray(arr.is_valid()))
+    assert isinstance(pa.__version__, str)
