@@ -1,21 +1,29 @@
 #!/usr/bin/env python3
-"""Decode throughput of the MI355X Parquet column-chunk decoder.
+"""Decode throughput of the MI355X Parquet column-chunk decoder (libpqgpu).
 
-Workload (BASELINE.json configs[1], "C2"): optional INT32 column, 100M rows per
-file, ~10% nulls, RLE_DICTIONARY with D = 2^b entries for every index width
-b in {1, 2, 4, 8, 12, 16, 20} (one file per width, uniform index draws), data
-page V1, UNCOMPRESSED, 20 000 rows per page.  A step decodes all seven column
-chunks (700M slots) in one batched call, inputs resident in HBM.
+Headline (BASELINE.json configs[1], "C2"): optional INT32 column, 100M rows per
+file, ~10% nulls, RLE_DICTIONARY with D = 2^b entries for every index width b in
+{1, 2, 4, 8, 12, 16, 20} (one file per width), data page V1, UNCOMPRESSED,
+20 000 rows per page.  A step decodes all seven column chunks (700M slots) in
+one batched call, inputs resident in HBM.
 
-Metric: decoded GB/s of uncompressed output (values[:nn] x 4 B + 1 B per
-def level), whole job = Σ over ranks / max time over ranks.  One process per
-GPU; row groups are independent, so ranks share nothing on the data path
-(weak scaling, no collective besides the timing barrier).
+Sub-results (same line, "configs"): C1 (required int64 PLAIN, 10M rows), C3
+(int64 DELTA_BINARY_PACKED, V2, SNAPPY, 200M rows), C4 (STRING dictionary +
+PLAIN fallback, SNAPPY, 50M rows) and one C5 shard (8 row groups x 15.625M rows
+of LIST<double> + 8 mixed columns).  Each carries its own roofline (dominant
+stage + whole pipeline) and CPU baseline.
 
-Prints ONE JSON line (rank 0).  Outputs are verified bit-exact against the
-generator's arrays after timing; the CPU baseline is the oracle (the C++
-restatement of parquet-go's decode, single thread like parquet-go's reader)
-timed on a bounded sample.
+Multi-GPU (one process per GPU, weak scaling): the data set has 8N C5 row
+groups and N C2 row groups per width; rank r decodes the row groups
+pqgpu.shard assigns it (RG i -> rank floor(i N / R)).  No collective touches
+the data path: only the timing barrier and the MAX of the elapsed time.
+
+Metric: decoded GB/s of uncompressed output (SURVEY §8d B_out: values, 1 B per
+level per slot, string chars + 4 B offsets), whole job = sum over ranks / max
+time over ranks.  Outputs are verified bit-exact against the generator's
+arrays after timing.  The CPU baseline is the oracle (the C++ restatement of
+parquet-go's decode) timed on a bounded sample: one thread (parquet-go's
+one-goroutine FileReader) and a pool of host threads over independent chunks.
 """
 import argparse
 import ctypes as C
@@ -34,23 +42,388 @@ for p in (ROOT, os.path.join(ROOT, "parquet-go_amd")):
 METRIC = "decoded GB/s (uncompressed output) per GPU & node at 1/2/4/8; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 STAGES = ["scan", "list", "snappy", "setup", "walk", "levels", "nn_scan", "values", "strings", "finalize"]
+PROFILE_TAG = "r02"
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(kernel, args):
-    """HBM bytes per launch of `kernel` from the committed PMC passes
-    (profiles/r01_pmc_traffic.json, made by tools/pmc_traffic.py from two
-    rocprofv3 --pmc runs of this same workload), or None for other workloads."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_traffic.json")
-    if args.rows != 100_000_000 or args.bits != "1,2,4,8,12,16,20" or not os.path.exists(path):
+def host_cores():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))  # the GPU box grants 16 host threads per GPU
+
+
+# ---------------------------------------------------------------- workloads
+class Workload:
+    """A set of files and the chunk jobs of one step, plus a verifier."""
+
+    def __init__(self, key, desc, files, dtype):
+        self.key, self.desc, self.dtype = key, desc, dtype
+        self.files = files  # list of (ParquetFile, [(rg, col)], expected)
+        self.devs = []
+
+
+def gen_workload(key, args, rank, world):
+    import pqgpu
+    from gen import pqwrite as W
+    from pqgpu import shard
+    t0 = time.time()
+    files = []
+    if key == "c2":
+        rgs = list(shard.row_groups_for_rank(world, rank, world))  # N row groups per width
+        bits_list = [int(b) for b in args.bits.split(",")]
+        for rg in rgs:
+            for bits, data, exp in W.config_c2_family(rows=args.rows, bits_list=bits_list, seed=2 + rg):
+                files.append((pqgpu.ParquetFile(data), [(0, 0)], ("c2", exp)))
+        desc = ("C2: optional INT32, %d rows x %d dictionary widths (b=%s), ~10%% nulls, RLE_DICTIONARY, V1, "
+                "UNCOMPRESSED, 20000 rows/page" % (args.rows, len(bits_list), args.bits))
+        dtype = "int32"
+    elif key == "c1":
+        data, info = W.config_c1(rows=args.c1_rows)
+        files.append((pqgpu.ParquetFile(data), [(0, 0)], ("flat", [info["values"]])))
+        desc = "C1: required INT64, %d rows, PLAIN, UNCOMPRESSED, 1 RG, V1, 20000 rows/page" % args.c1_rows
+        dtype = "int64"
+    elif key == "c3":
+        data, info = W.config_c3(rows=args.c3_rows)
+        files.append((pqgpu.ParquetFile(data), [(0, 0)], ("flat", [info["values"]])))
+        desc = ("C3: INT64 timestamps, %d rows, DELTA_BINARY_PACKED (128/4x32), V2, SNAPPY, 20000 rows/page"
+                % args.c3_rows)
+        dtype = "int64"
+    elif key == "c4":
+        data, info = W.config_c4(rows=args.c4_rows)
+        files.append((pqgpu.ParquetFile(data), [(0, 0)], ("str", info)))
+        desc = ("C4: required STRING, %d rows, 65536-word vocabulary (len U[4,32], Zipf 1.1), dictionary pages "
+                "then PLAIN fallback after 1 MiB, SNAPPY, V1, 20000 rows/page" % args.c4_rows)
+        dtype = "u8"
+    elif key == "c5":
+        R = 8 * world  # 8 row groups per GPU (64 at 8 GPUs, the C5 file)
+        rgs = list(shard.row_groups_for_rank(R, rank, world))
+        data, info = W.config_c5(row_groups=rgs, rows_per_rg=args.c5_rows_per_rg)
+        pf = pqgpu.ParquetFile(data)
+        files.append((pf, [(i, c) for i in range(len(rgs)) for c in range(pf.num_columns)], ("c5", info)))
+        desc = ("C5 shard: row groups %s of %d (RG i -> GPU floor(i*%d/%d)), %d rows each: LIST<double> + int32, "
+                "int64 DBP, double, float, int96, optional int32 dict, string dict, int64 SNAPPY"
+                % (rgs, R, world, R, args.c5_rows_per_rg))
+        dtype = "mixed"
+    else:
+        raise ValueError(key)
+    log("rank %d: %s generated in %.1fs (%.1f MB)" % (rank, key, time.time() - t0,
+                                                      sum(len(f[0].data) for f in files) / 1e6))
+    return Workload(key, desc, files, dtype)
+
+
+# ---------------------------------------------------------------- byte accounting
+def _level_sections(pf, meta, pg, desc):
+    """(level bytes, value-section bytes) of a data page, from its header and,
+    for V1 pages, the u32 length prefixes of the level sections."""
+    if pg.page_type == 3:
+        lv = pg.def_len + pg.rep_len
+        return lv, pg.uncompressed_size - lv
+    if desc.max_def == 0 and desc.max_rep == 0:
+        return 0, pg.uncompressed_size
+    at = meta.start + pg.payload_offset
+    body = pf.data[at:at + pg.compressed_size]
+    if meta.codec != 0:
+        import pyarrow as pa
+        body = pa.decompress(body, decompressed_size=pg.uncompressed_size, codec="snappy").to_pybytes()
+    pos = 0
+    for present in (desc.max_rep > 0, desc.max_def > 0):
+        if present:
+            pos += 4 + int.from_bytes(body[pos:pos + 4], "little")
+    return pos, pg.uncompressed_size - pos
+
+
+def account(wl, dec, res):
+    """B_in/B_out of the step and algorithmic bytes per stage."""
+    b_in = b_out = 0
+    st = dict.fromkeys(STAGES, 0)
+    ji = 0
+    for pf, specs, _ in wl.files:
+        for (rg, col) in specs:
+            r = res[ji]
+            meta = pf.chunk_meta(rg, col)
+            desc = pf.columns[col].desc
+            b_in += meta.total_compressed_size
+            nlev = (desc.max_def > 0) + (desc.max_rep > 0)
+            slots_out = r.num_slots * nlev
+            if r.value_width:
+                vout = r.num_values * r.value_width
+                b_out += vout + slots_out
+            else:
+                vout = r.values_bytes + (r.num_values + 1) * 8  # chars + int64 offsets written
+                b_out += r.values_bytes + (r.num_values + 1) * 4 + slots_out
+            st["scan"] += meta.total_compressed_size
+            lev_in = val_in = dict_in = 0
+            for pg in dec.pages(ji):
+                if pg.page_type == 2:
+                    dict_in += pg.uncompressed_size
+                    continue
+                lv, vb = _level_sections(pf, meta, pg, desc)
+                lev_in += lv
+                val_in += vb
+                if pg.encoding == 8:
+                    st["walk"] += vb
+                if meta.codec != 0:
+                    lv2 = lv if pg.page_type == 3 else 0
+                    st["snappy"] += pg.compressed_size - lv2 + pg.uncompressed_size - lv2
+            st["walk"] += lev_in
+            st["levels"] += lev_in + slots_out
+            st["values" if r.value_width else "strings"] += val_in + dict_in + vout
+            ji += 1
+    return b_in, b_out, st
+
+
+# ---------------------------------------------------------------- verification
+def verify(wl, dec, res):
+    ok = True
+    ji = 0
+    for pf, specs, (kind, exp) in wl.files:
+        for (rg, col) in specs:
+            r = res[ji]
+            ji += 1
+            if r.status != 0:
+                return False
+            if kind == "c2":
+                defs, vals = exp
+                ok &= np.array_equal(dec.d2h(r.def_levels, r.num_slots), defs)
+                ok &= np.array_equal(dec.d2h(r.values, r.values_bytes).view(vals.dtype), vals)
+            elif kind == "flat":
+                v = exp[0]
+                ok &= np.array_equal(dec.d2h(r.values, r.values_bytes).view(v.dtype), v)
+            elif kind == "str":
+                ok &= np.array_equal(dec.d2h(r.offsets, (r.num_values + 1) * 8, np.int64), exp["offsets"])
+                ok &= np.array_equal(dec.d2h(r.values, r.values_bytes), exp["chars"])
+            elif kind == "c5":
+                e = exp["parts"][rg][pf.columns[col].path.decode().split(".")[0]]
+                if "offsets" in e:
+                    ok &= np.array_equal(dec.d2h(r.offsets, (r.num_values + 1) * 8, np.int64), e["offsets"])
+                ok &= np.array_equal(dec.d2h(r.values, r.values_bytes), np.ascontiguousarray(e["values"]).view(np.uint8))
+                if e.get("def_levels") is not None:
+                    ok &= np.array_equal(dec.d2h(r.def_levels, r.num_slots), e["def_levels"])
+                if e.get("rep_levels") is not None:
+                    ok &= np.array_equal(dec.d2h(r.rep_levels, r.num_slots), e["rep_levels"])
+    return bool(ok)
+
+
+# ---------------------------------------------------------------- CPU baseline
+def cpu_baseline(wl, seconds):
+    """The oracle (C++ restatement of parquet-go's readPages/readPageData) on a
+    bounded sample of the workload's chunks: one thread, then a thread pool
+    over independent chunks (ctypes releases the GIL during the call)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import pyoracle as O
+    from pqgpu import abi
+    OL = O.lib()
+    jobs = []
+    for pf, specs, _ in wl.files:
+        for (rg, col) in specs:
+            jobs.append(pf.host_job(rg, col)[0])
+
+    def run(job):
+        r = abi.ChunkResult()
+        pages = (abi.PageInfo * 1)()
+        n = C.c_int(0)
+        OL.pqo_decode_chunk(C.byref(job), C.byref(r), pages, 1, C.byref(n))
+        lev = r.num_slots * ((job.col.max_def > 0) + (job.col.max_rep > 0))
+        b = lev + (r.num_values * r.value_width if r.value_width else r.values_bytes + (r.num_values + 1) * 4)
+        OL.pqo_free_result(C.byref(r))
+        return b
+
+    done, t1, k = 0, 0.0, 0
+    while k < len(jobs) and t1 < seconds / 2:
+        t = time.perf_counter()
+        done += run(jobs[k])
+        t1 += time.perf_counter() - t
+        k += 1
+    single = done / t1 / 1e9
+    cores = host_cores()
+    sample = [jobs[i % len(jobs)] for i in range(min(len(jobs), max(cores, k)))]
+    t = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=cores) as ex:
+        pool_bytes = sum(ex.map(run, sample))
+    tp = time.perf_counter() - t
+    used = min(cores, len(sample))
+    return ({"value": round(single, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+             "sample": "oracle (C++ restatement of parquet-go readPages/readPageData) on %d of %d chunks, one thread "
+                       "like parquet-go's one-goroutine FileReader; %.1fs" % (k, len(jobs), t1)},
+            {"value": round(pool_bytes / tp / 1e9, 4), "unit": "GB/s", "cores": used, "kind": "port",
+             "sample": "oracle on %d chunks over a pool of %d host threads (independent column chunks); %.1fs"
+                       % (len(sample), used, tp)})
+
+
+# ---------------------------------------------------------------- PMC traffic (committed passes)
+STAGE_KERNELS = {"scan": ["k_page_cands", "k_cand_parse", "k_tile_scan", "k_cand_link", "k_page_chain",
+                          "k_scan_pages"], "list": ["k_page_list"], "snappy": ["k_snappy"], "setup": ["k_page_setup"],
+                 "walk": ["k_hybrid_walk"], "levels": ["k_levels_expand"], "nn_scan": ["k_nn_scan"],
+                 "values": ["k_values"], "strings": ["k_str_dict", "k_str_plain", "k_str_count", "k_char_scan",
+                                                  "k_str_copy"],
+                 "finalize": ["k_finalize"]}
+
+
+def pmc_traffic(key, kernels, workload):
+    """HBM bytes per step of a stage's kernels from the committed PMC passes
+    (profiles/<tag>_pmc_<config>.json, tools/pmc_traffic.py), if they were taken
+    on this same workload; else None."""
+    path = os.path.join(ROOT, "profiles", "%s_pmc_%s.json" % (PROFILE_TAG, key))
+    if not os.path.exists(path):
         return None
-    ks = json.load(open(path))["kernels"]
-    # the values stage is k_values<1> (4-byte dictionaries) + k_values<0> (all else)
-    names = [k for k in ks if k.split("<")[0] == "pqg::" + kernel]
-    return sum(ks[k]["traffic"] for k in names) or None
+    d = json.load(open(path))
+    if d.get("workload") != workload:
+        return None
+    tot = sum(v["traffic"] for k, v in d["kernels"].items() if any(k.startswith("pqg::" + p) for p in kernels))
+    return tot or None
+
+
+# ---------------------------------------------------------------- run one workload
+def run_workload(wl, dec, args, steps, warmup, barrier, dist, world, rank, cpu_seconds):
+    import pqgpu
+    from pqgpu import abi
+    L = dec.L
+    jobs = []
+    for pf, specs, _ in wl.files:
+        dev = dec.upload(pf.data)
+        wl.devs.append(dev)
+        for (rg, col) in specs:
+            jobs.append(pqgpu.device_job(pf, rg, col, dev))
+    n = len(jobs)
+    arr = (abi.ChunkJob * n)(*jobs)
+    res = (abi.ChunkResult * n)()
+    tmp = (C.c_float * 16)()
+
+    def step():
+        rc = L.pqg_decode_chunks(dec.ctx, arr, n, res)
+        if rc != 0:
+            raise RuntimeError("decode failed: %d" % rc)
+
+    for _ in range(max(warmup, 1)):
+        step()
+    bad = [abi.status_name(res[i].status) for i in range(n) if res[i].status != 0]
+    assert not bad, "%s: %s" % (wl.key, bad)
+    stage_acc = np.zeros(len(STAGES))
+    barrier()
+    t_start = time.perf_counter()
+    for _ in range(steps):
+        step()
+        k = L.pqg_last_timings(dec.ctx, tmp, 16)
+        stage_acc += np.array([tmp[i] for i in range(1, min(k, 1 + len(STAGES)))])
+    t_end = time.perf_counter()
+    barrier()
+    elapsed = t_end - t_start
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    b_in, b_out, alg = account(wl, dec, res)
+    stage_ms = stage_acc / steps
+    dev_ms = float(stage_ms.sum())
+    dom = int(np.argmax(stage_ms))
+    dom_name = STAGES[dom]
+    achieved = alg[dom_name] / (stage_ms[dom] * 1e-3) / 1e9 if stage_ms[dom] > 0 else 0.0
+    out = {
+        "workload": wl.desc,
+        "value": round(b_out * world / elapsed * steps / 1e9, 3),
+        "unit": "GB/s",
+        "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "steps": steps,
+        "chunks_per_step": n,
+        "bytes_in": b_in,
+        "bytes_out": b_out,
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "stage " + dom_name + " (" + "+".join(STAGE_KERNELS[dom_name]) + ")",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": pmc_traffic(wl.key, STAGE_KERNELS[dom_name], wl.desc),
+            "alg_bytes_per_launch": alg[dom_name],
+            "kernel_ms": round(float(stage_ms[dom]), 4),
+            "pipeline_device_ms": round(dev_ms, 4),
+            "pipeline_frac": round((b_in + b_out) / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dev_ms else 0.0,
+            "stage_ms": {s: round(float(x), 4) for s, x in zip(STAGES, stage_ms)},
+            "stage_alg_bytes": alg,
+        },
+    }
+    if not args.no_verify:
+        out["verified_bit_exact"] = verify(wl, dec, res)
+        if not out["verified_bit_exact"]:
+            log("VERIFY FAILED:", wl.key)
+    if rank == 0 and not args.no_cpu:
+        single, pool = cpu_baseline(wl, cpu_seconds)
+        out["cpu_baseline"] = single
+        out["cpu_baseline_all_cores"] = pool
+    return out, res
+
+
+def k8_c2(dec, wl, res, args):
+    """K8 (pqg_assemble) on the first C2 chunk's device arrays: validity bitmap +
+    spaced values.  Host-timed including the sync; not part of `value`."""
+    from pqgpu import abi
+    L = dec.L
+    r = res[0]
+    a, vb, sb, _ = dec.assemble(r.def_levels, r.rep_levels, r.values, r.num_slots, 1, 0, 4,
+                                validity=True, spaced=True, offsets=False)
+    reps = 5
+    t1 = time.perf_counter()
+    for _ in range(reps):
+        rc = L.pqg_assemble(dec.ctx, C.byref(a))
+        assert rc == 0, abi.status_name(rc)
+    ms = (time.perf_counter() - t1) / reps * 1e3
+    n = r.num_slots
+    nbytes = n + r.num_values * 4 + n * 4 + (n + 7) // 8
+    out = {"kernels": "k_asm_count+k_asm_scan+k_asm_write<4>", "slots": n, "ms": round(ms, 4), "alg_bytes": nbytes,
+           "achieved_GBs": round(nbytes / (ms * 1e-3) / 1e9, 1),
+           "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "timer": "host wall, incl. sync"}
+    if not args.no_verify:
+        defs, vals = wl.files[0][2][1]
+        valid = defs == 1
+        sp = dec.d2h(sb, n * 4).view(np.int32)
+        bm = np.unpackbits(dec.d2h(vb, (n + 7) // 8), bitorder="little")[:n].astype(bool)
+        out["verified"] = bool(np.array_equal(bm, valid) and np.array_equal(sp[valid], vals)
+                               and not sp[~valid].any() and a.num_valid == int(valid.sum()))
+    dec.free(vb)
+    dec.free(sb)
+    return out
+
+
+def k8_list_c5(dec, wl, res, args):
+    """K8 list export (pqg_assemble_list) of the C5 shard's LIST<double> chunks."""
+    from pqgpu import abi
+    L = dec.L
+    pf, specs, (_, info) = wl.files[0]
+    idx = [i for i, (rg, col) in enumerate(specs) if col == 0]
+    tot_ms, tot_bytes, ok = 0.0, 0, True
+    for i in idx:
+        r = res[i]
+        a, lvp, lop, evp, vvp = dec.assemble_list(r.def_levels, r.rep_levels, r.values, r.num_slots, 3, 1, 2, 8)
+        t1 = time.perf_counter()
+        rc = L.pqg_assemble_list(dec.ctx, C.byref(a))
+        assert rc == 0, abi.status_name(rc)
+        tot_ms += (time.perf_counter() - t1) * 1e3
+        n = r.num_slots
+        tot_bytes += 2 * n + r.num_values * 8 + (a.num_rows + 1) * 4 + (a.num_rows + 7) // 8 + \
+            (a.num_elements + 7) // 8 + a.num_elements * 8
+        if not args.no_verify:
+            rows = a.num_rows
+            ok &= rows == info["rows_per_rg"] and a.num_valid == r.num_values
+            lo = dec.d2h(lop, (rows + 1) * 4, np.int32)
+            e = info["parts"][specs[i][0]]["lst"]
+            starts = np.flatnonzero(e["rep_levels"] == 0)
+            el = e["def_levels"] >= 2
+            ok &= bool(np.array_equal(lo, np.r_[np.cumsum(el)[starts] - el[starts], el.sum()].astype(np.int32)))
+        for p in (lvp, lop, evp, vvp):
+            dec.free(p)
+    out = {"kernels": "k_list_count+k_list_scan+k_list_write<8>", "chunks": len(idx), "ms": round(tot_ms, 4),
+           "alg_bytes": tot_bytes, "achieved_GBs": round(tot_bytes / (tot_ms * 1e-3) / 1e9, 1),
+           "frac": round(tot_bytes / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "timer": "host wall, incl. sync"}
+    if not args.no_verify:
+        out["verified"] = bool(ok)
+    return out
 
 
 def main():
@@ -58,11 +431,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--rows", type=int, default=100_000_000, help="C2 rows per file")
     ap.add_argument("--bits", type=str, default="1,2,4,8,12,16,20")
+    ap.add_argument("--configs", type=str, default="c1,c3,c4,c5", help="sub-results besides the C2 headline")
+    ap.add_argument("--sub-steps", type=int, default=5)
+    ap.add_argument("--c1-rows", type=int, default=10_000_000)
+    ap.add_argument("--c3-rows", type=int, default=200_000_000)
+    ap.add_argument("--c4-rows", type=int, default=50_000_000)
+    ap.add_argument("--c5-rows-per-rg", type=int, default=15_625_000)
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bound on the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=16.0, help="bound on the headline CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--only", type=str, default="", help="profiling: run one config alone and print its result")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -75,203 +455,72 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    import pqgpu
-    from gen import pqwrite as W
-    from pqgpu import abi
-
-    bits_list = [int(b) for b in args.bits.split(",")]
-    t0 = time.time()
-    files = list(W.config_c2_family(rows=args.rows, bits_list=bits_list))
-    log("rank %d: generated %d files in %.1fs (%.1f MB)" % (rank, len(files), time.time() - t0,
-                                                            sum(len(f[1]) for f in files) / 1e6))
-    dec = pqgpu.GpuDecoder(local)
-    jobs, pfs = [], []
-    b_in = 0
-    for bits, data, _ in files:
-        pf = pqgpu.ParquetFile(data)
-        dev = dec.upload(pf.data)
-        for rg in range(pf.num_row_groups):
-            jobs.append(pqgpu.device_job(pf, rg, 0, dev))
-            b_in += pf.chunk_meta(rg, 0).total_compressed_size
-        pfs.append(pf)
-    n_jobs = len(jobs)
-    arr = (abi.ChunkJob * n_jobs)(*jobs)
-    res = (abi.ChunkResult * n_jobs)()
-    L = dec.L
-
-    def step():
-        rc = L.pqg_decode_chunks(dec.ctx, arr, n_jobs, res)
-        if rc != 0:
-            raise RuntimeError("decode failed: %d" % rc)
-
-    stage_acc = np.zeros(len(STAGES))
-    tmp = (C.c_float * 16)()
-
-    def stage_times():
-        k = L.pqg_last_timings(dec.ctx, tmp, 16)
-        return np.array([tmp[i] for i in range(1, min(k, 1 + len(STAGES)))])
-
-    for _ in range(max(args.warmup, 1)):
-        step()
-    for i in range(n_jobs):
-        assert res[i].status == 0, abi.status_name(res[i].status)
-
     def barrier():
         if dist is not None:
             import torch
             torch.cuda.synchronize()
             dist.barrier()
 
-    barrier()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        stage_acc += stage_times()
-    t_end = time.perf_counter()
-    barrier()
-    elapsed = t_end - t_start
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    import pqgpu
+    dec = pqgpu.GpuDecoder(local)
 
-    # ---- bytes
-    nn_total = sum(res[i].num_values for i in range(n_jobs))
-    slots_total = sum(res[i].num_slots for i in range(n_jobs))
-    b_out = nn_total * 4 + slots_total * 1
-    value = b_out * world * args.steps / elapsed / 1e9
-    ms_per_step = elapsed / args.steps * 1e3
-    stage_ms = stage_acc / args.steps
-    dev_ms = float(stage_ms.sum())
+    def release(wl):
+        for d in wl.devs:
+            dec.free(d)
+        wl.devs = []
 
-    # dominant kernel: values (dictionary gather) or levels
-    pages_info = [dec.pages(i) for i in range(n_jobs)]
-    val_in = sum(p.uncompressed_size for pl in pages_info for p in pl if p.page_type == 0)
-    dom = int(np.argmax(stage_ms))
-    # exact level-stream sizes: read the u32 length prefix of each V1 page body
-    def_stream = 0
-    for pf, pl, j in zip(pfs, pages_info, jobs):
-        m = pf.chunk_meta(0, 0)
-        for p in pl:
-            if p.page_type == 0:
-                at = m.start + p.payload_offset
-                def_stream += 4 + int.from_bytes(pf.data[at:at + 4], "little")
-    alg = {
-        "levels": def_stream + slots_total,                      # def-level stream in, 1 B/slot out
-        "values": (val_in - def_stream) + nn_total * 4,          # index stream in, values out
-        "scan": 0, "list": 0, "snappy": 0, "nn_scan": 0, "finalize": 0,
-    }
-    dom_name = STAGES[dom]
-    dom_bytes = alg.get(dom_name, 0)
-    achieved = dom_bytes / (stage_ms[dom] * 1e-3) / 1e9 if stage_ms[dom] > 0 else 0.0
-    pipeline_gbs = (b_in + b_out) / (dev_ms * 1e-3) / 1e9 if dev_ms > 0 else 0.0
+    if args.only:  # profiling runs (tools/gpu_profile.sh): one workload, its own JSON line
+        w = gen_workload(args.only, args, rank, world)
+        sub, _ = run_workload(w, dec, args, args.steps, args.warmup, barrier, dist, world, rank, 6.0)
+        if rank == 0:
+            print(json.dumps({"only": args.only, **sub}), flush=True)
+        release(w)
+        dec.close()
+        return
 
-    # ---- verify bit-exact against the generator's arrays (size-independent check)
-    verified = None
-    if not args.no_verify:
-        ok = True
-        for i, (bits, data, (defs, vals)) in enumerate(files):
-            r = res[i]
-            got_d = dec.d2h(r.def_levels, r.num_slots)
-            got_v = dec.d2h(r.values, r.values_bytes).view(np.int32)
-            ok &= r.num_slots == len(defs) and np.array_equal(got_d, defs) and np.array_equal(got_v, vals)
-        verified = bool(ok)
-        if not ok:
-            log("VERIFY FAILED")
-
-    # ---- K8 (pqg_assemble) on chunk 0's decoded arrays: validity bitmap + spaced
-    # values (row offsets are trivial for a flat column).  Not part of `value`.
-    k8 = None
-    if rank == 0:
-        r = res[0]
-        a, vb, sb, _ = dec.assemble(r.def_levels, r.rep_levels, r.values, r.num_slots, 1, 0, 4,
-                                    validity=True, spaced=True, offsets=False)
-        reps = 5
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            rc = L.pqg_assemble(dec.ctx, C.byref(a))
-            assert rc == 0, abi.status_name(rc)
-        k8_ms = (time.perf_counter() - t1) / reps * 1e3
-        n = r.num_slots
-        k8_bytes = n + r.num_values * 4 + n * 4 + (n + 7) // 8
-        k8 = {"kernels": "k_asm_count+k_asm_scan+k_asm_write<4>", "slots": n, "ms": round(k8_ms, 4),
-              "alg_bytes": k8_bytes, "achieved_GBs": round(k8_bytes / (k8_ms * 1e-3) / 1e9, 1),
-              "frac": round(k8_bytes / (k8_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "timer": "host wall, incl. sync"}
-        if not args.no_verify:
-            defs, vals = files[0][2]
-            valid = defs == 1
-            sp = dec.d2h(sb, n * 4).view(np.int32)
-            bm = np.unpackbits(dec.d2h(vb, (n + 7) // 8), bitorder="little")[:n].astype(bool)
-            k8["verified"] = bool(np.array_equal(bm, valid) and np.array_equal(sp[valid], vals)
-                                  and not sp[~valid].any() and a.num_valid == int(valid.sum()))
-        dec.free(vb)
-        dec.free(sb)
-
-    # ---- CPU baseline: oracle (single thread) on a bounded sample
-    cpu = None
-    if rank == 0 and not args.no_cpu:
-        from oracle import pyoracle as O
-        OL = O.lib()
-        done_bytes, t_cpu, names = 0, 0.0, []
-        for bits, data, _ in files:
-            pf = pqgpu.ParquetFile(data)
-            job, _ = pf.host_job(0, 0)
-            r = abi.ChunkResult()
-            pages = (abi.PageInfo * 1)()
-            n = C.c_int(0)
-            t1 = time.perf_counter()
-            OL.pqo_decode_chunk(C.byref(job), C.byref(r), pages, 1, C.byref(n))
-            t_cpu += time.perf_counter() - t1
-            done_bytes += r.num_values * 4 + r.num_slots
-            OL.pqo_free_result(C.byref(r))
-            names.append("b=%d" % bits)
-            if t_cpu >= args.cpu_seconds:
-                break
-        cpu = {"value": round(done_bytes / t_cpu / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-               "sample": "oracle (C++ restatement of parquet-go readPages/readPageData) on %d of the %d C2 files "
-                         "(%s; %d rows each), single thread like parquet-go's one-goroutine FileReader; %.1fs"
-                         % (len(names), len(files), ",".join(names), args.rows, t_cpu)}
+    wl = gen_workload("c2", args, rank, world)
+    head, res = run_workload(wl, dec, args, args.steps, args.warmup, barrier, dist, world, rank, args.cpu_seconds)
+    k8 = k8_c2(dec, wl, res, args) if rank == 0 else None
+    release(wl)
+    del wl
+    subs = {}
+    for key in [k for k in args.configs.split(",") if k]:
+        w = gen_workload(key, args, rank, world)
+        sub, sres = run_workload(w, dec, args, args.sub_steps, 1, barrier, dist, world, rank, 6.0)
+        if key == "c5" and rank == 0:
+            sub["k8_list_export"] = k8_list_c5(dec, w, sres, args)
+        subs[key + ("_shard" if key == "c5" else "")] = sub
+        release(w)
+        del w
 
     if rank == 0:
         out = {
             "metric": METRIC,
-            "value": round(value, 3),
+            "value": head["value"],
             "unit": "GB/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic",
             "config": {
-                "workload": "C2: optional INT32, %d rows x %d dictionary widths (b=%s), ~10%% nulls, "
-                            "RLE_DICTIONARY, V1, UNCOMPRESSED, 20000 rows/page" % (args.rows, len(bits_list), args.bits),
-                "chunks_per_step": n_jobs,
-                "bytes_in": b_in,
-                "bytes_out": b_out,
-                "parallelism": "replicas: one process per GPU, independent row groups" if world > 1 else "single GPU",
+                "workload": head["workload"],
+                "chunks_per_step": head["chunks_per_step"],
+                "bytes_in": head["bytes_in"],
+                "bytes_out": head["bytes_out"],
+                "parallelism": ("row-group shards: one process per GPU, RG i -> GPU floor(i*N/R), no data-path "
+                                "collective" if world > 1 else "single GPU"),
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "k_%s" % dom_name,
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic("k_" + dom_name, args),
-                "alg_bytes_per_launch": dom_bytes,
-                "kernel_ms": round(float(stage_ms[dom]), 4),
-                "pipeline_device_ms": round(dev_ms, 4),
-                "pipeline_frac": round(pipeline_gbs / HBM_PEAK_GBS, 4),
-                "stage_ms": {n: round(float(x), 4) for n, x in zip(STAGES, stage_ms)},
-            },
-            "cpu_baseline": cpu,
-            "verified_bit_exact": verified,
+            "roofline": head["roofline"],
+            "cpu_baseline": head.get("cpu_baseline"),
+            "cpu_baseline_all_cores": head.get("cpu_baseline_all_cores"),
+            "verified_bit_exact": head.get("verified_bit_exact"),
             "k8_assemble": k8,
+            "configs": subs,
         }
         print(json.dumps(out), flush=True)
     dec.close()

@@ -116,7 +116,8 @@ def write_file(columns, num_rows, row_groups=1):
     rc = L.pqw_write_file(arr, len(columns), num_rows, row_groups, C.byref(out), C.byref(n))
     if rc != 0:
         raise ValueError("pqw_write_file failed: %d" % rc)
-    data = C.string_at(out, n.value)
+    # (ctypes.string_at takes a C int size: files past 2 GiB are copied via numpy)
+    data = np.ctypeslib.as_array(C.cast(out, C.POINTER(C.c_uint8)), shape=(n.value,)).tobytes()
     L.pqw_free(out)
     return data
 
@@ -165,7 +166,7 @@ def config_c1(rows=10_000_000, rows_per_page=20000, seed=1):
     """C1: required int64, PLAIN, UNCOMPRESSED, one row group, V1."""
     vals = splitmix64(seed, rows).view(np.int64)
     col = Column("c1", INT64, vals, rows_per_page=rows_per_page)
-    return write_file([col], rows), {"rows": rows}
+    return write_file([col], rows), {"rows": rows, "values": vals}
 
 
 def config_c2(rows=100_000_000, bits=8, null_frac=0.10, run_heavy=False, rows_per_page=20000, seed=2,
@@ -201,7 +202,7 @@ def config_c3(rows=200_000_000, rows_per_page=20000, seed=3, codec=SNAPPY):
     vals = np.int64(1_600_000_000_000_000) + np.cumsum(deltas)
     col = Column("ts", INT64, vals, encoding=DELTA_BINARY_PACKED, codec=codec, page_version=2,
                  rows_per_page=rows_per_page)
-    return write_file([col], rows), {"rows": rows}
+    return write_file([col], rows), {"rows": rows, "values": vals}
 
 
 def make_vocab(n, seed, lo=4, hi=32):
@@ -235,7 +236,7 @@ def config_c4(rows=50_000_000, vocab=65536, rows_per_page=20000, seed=4, dict_li
     out_chars = chars[idx]
     col = Column("s", BYTE_ARRAY, out_chars, offsets=out_offs, encoding=RLE_DICTIONARY, codec=codec,
                  rows_per_page=rows_per_page, dict_limit=dict_limit)
-    return write_file([col], rows), {"rows": rows}
+    return write_file([col], rows), {"rows": rows, "chars": out_chars, "offsets": out_offs}
 
 
 def config_c2_family(rows=100_000_000, bits_list=(1, 2, 4, 8, 12, 16, 20), null_frac=0.10, rows_per_page=20000,
@@ -356,4 +357,4 @@ def config_c5(row_groups=(0,), rows_per_rg=C5_ROWS_PER_RG, seed=5, rows_per_page
         Column("i64s", INT64, cat("i64s", "values"), codec=SNAPPY, rows_per_page=rows_per_page),
     ]
     data = write_file(cols, rows, row_groups=len(parts))
-    return data, {"rows": rows, "row_groups": list(row_groups), "rows_per_rg": rows_per_rg}
+    return data, {"rows": rows, "row_groups": list(row_groups), "rows_per_rg": rows_per_rg, "parts": parts}

@@ -147,6 +147,50 @@ __device__ __forceinline__ uint64_t extract_bits64(P p, int64_t n, int64_t valid
   return w == 64 ? v : (v & ((1ull << w) - 1));
 }
 
+// ---------------------------------------------------------------------------
+// Wave-cooperative byte copy, any alignment on either side: 16-byte aligned
+// destination granules (one dwordx4 store per lane), each funnel-shifted out of
+// two aligned 16-byte source granules; ragged head and tail bytewise.  Only
+// granules holding a source byte are read (mapped memory).
+// ---------------------------------------------------------------------------
+template <int Q>
+__device__ __forceinline__ void wave_copy_body(PQG_G uint8_t* db, uintptr_t sbase, uint32_t r, int64_t body) {
+  const int lane = lane_id();
+  for (int64_t g = (int64_t)lane * 16; g < body; g += 64 * 16) {
+    const uint4 a = ldg16(sbase + g);
+    uint4 b = a;
+    if (Q != 0 || r != 0) b = ldg16(sbase + g + 16);
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint4 o;
+    o.x = __builtin_amdgcn_alignbit(w[Q + 1], w[Q], r);
+    o.y = __builtin_amdgcn_alignbit(w[Q + 2], w[Q + 1], r);
+    o.z = __builtin_amdgcn_alignbit(w[Q + 3], w[Q + 2], r);
+    o.w = __builtin_amdgcn_alignbit(w[Q + 4 < 8 ? Q + 4 : 7], w[Q + 3], r);
+    stg16((uintptr_t)(db + g), o);
+  }
+}
+
+__device__ __forceinline__ void wave_copy(PQG_G uint8_t* dst, const PQG_G uint8_t* src, int64_t nbytes) {
+  if (nbytes <= 0) return;
+  const int lane = lane_id();
+  int64_t head = (int64_t)((16 - ((uintptr_t)dst & 15)) & 15);
+  if (head > nbytes) head = nbytes;
+  if (lane < head) dst[lane] = src[lane];
+  const int64_t body = (nbytes - head) & ~(int64_t)15;
+  PQG_G uint8_t* db = dst + head;
+  const uintptr_t sa = (uintptr_t)(src + head);
+  const uintptr_t sbase = sa & ~(uintptr_t)15;
+  const uint32_t q = (uint32_t)(sa >> 2) & 3, r = (uint32_t)(sa & 3) * 8;
+  switch (q) {
+    case 0: wave_copy_body<0>(db, sbase, r, body); break;
+    case 1: wave_copy_body<1>(db, sbase, r, body); break;
+    case 2: wave_copy_body<2>(db, sbase, r, body); break;
+    default: wave_copy_body<3>(db, sbase, r, body); break;
+  }
+  const int64_t t0 = head + body;
+  if (t0 + lane < nbytes) dst[t0 + lane] = src[t0 + lane];
+}
+
 // In-kernel phase timing (diagnostic builds only: -DPQG_PROFILE).  Lane 0
 // adds s_memtime deltas into pqg_prof[slot]; pqg_debug_counters reads them.
 #ifdef PQG_PROFILE

@@ -36,6 +36,7 @@ __global__ void k_page_chain(JobDev* jobs, PageDev* pages, const Cand* cands, co
                              const int* idx2slot, const int* ok2slot, int* order);
 __global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs);
 __global__ void k_page_list(JobDev* jobs, int n_jobs, int* list, int list_cap, int* total, int* queues);
+template <int RING, int KIND>
 __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                          uint8_t* scratch);
 __global__ void k_page_setup(JobDev* jobs, PageDev* pages, const int* list, const int* total, uint8_t* scratch,
@@ -53,16 +54,19 @@ __global__ void k_finalize(JobDev* jobs, int n_jobs, PageDev* pages);
 __global__ void k_str_dict(JobDev* jobs, PageDev* pages, int64_t* doffs_arena);
 __global__ void k_str_count(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                             int64_t* offs_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks);
+__global__ void k_str_plain(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                            int64_t* offs_arena);
 __global__ void k_char_scan(JobDev* jobs, PageDev* pages, int64_t* offs_arena);
-__global__ void k_str_write(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
-                            uint8_t* value_arena, int64_t* offs_arena, const HStream* streams, const RunEnt* runs,
-                            const BlockDesc* blks);
+__global__ void k_str_copy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                           uint8_t* value_arena, int64_t* offs_arena);
 }  // namespace pqg
 
 #ifdef PQG_PROFILE
 namespace pqg {
 int prof_read_values(unsigned long long* out);
 int prof_read_levels(unsigned long long* out);
+int prof_read_strings(unsigned long long* out);
+int prof_read_snappy(unsigned long long* out);
 }  // namespace pqg
 #endif
 
@@ -360,7 +364,7 @@ static int launch_pipeline(pqg_ctx* c) {
   // page-queue kernels: one wave per page; enough waves per SIMD to hide the
   // dependent HBM reads of the run walks (bounded by VGPRs / LDS per kernel)
   const int waves = c->num_cus * 20;
-  const int snappy_waves = c->num_cus * 4;  // 33 KiB LDS each
+  const int snappy_waves = c->num_cus * 4;  // 33 KiB LDS each (65 KiB for the large-block instance)
   hipStream_t s = c->stream;
   if (c->timed) hipEventRecord(c->ev[0], s);
   const int64_t nt = c->total_tiles;
@@ -391,8 +395,12 @@ static int launch_pipeline(pqg_ctx* c) {
   if (c->timed) hipEventRecord(c->ev[2], s);
   bool any_comp = false;
   for (int i = 0; i < n; i++) any_comp |= c->cur[(size_t)i].col.codec != PQG_CODEC_UNCOMPRESSED;
-  if (any_comp)
-    hipLaunchKernelGGL(k_snappy, dim3(snappy_waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 8, scratch);
+  if (any_comp) {
+    hipLaunchKernelGGL((k_snappy<32768, 0>), dim3(snappy_waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 8,
+                       scratch);
+    hipLaunchKernelGGL((k_snappy<65536, 1>), dim3(c->num_cus * 2), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 21,
+                       scratch);
+  }
   if (c->timed) hipEventRecord(c->ev[3], s);
   HStream* streams = (HStream*)c->streams.p;
   RunEnt* runs = (RunEnt*)c->runs.p;
@@ -419,12 +427,14 @@ static int launch_pipeline(pqg_ctx* c) {
   if (c->timed) hipEventRecord(c->ev[8], s);
   if (c->any_var) {
     int64_t* offs = (int64_t*)c->offs_arena.p;
-    hipLaunchKernelGGL(k_str_dict, dim3(n), dim3(64), 0, s, jobs, pages, (int64_t*)c->doffs_arena.p);
+    hipLaunchKernelGGL(k_str_dict, dim3(n), dim3(512), 0, s, jobs, pages, (int64_t*)c->doffs_arena.p);
+    hipLaunchKernelGGL(k_str_plain, dim3(c->num_cus * 4), dim3(512), 0, s, jobs, pages, vlists + 2 * lcap, ctr + 14,
+                       ctr + 19, offs);
     hipLaunchKernelGGL(k_str_count, dim3(waves), dim3(64), 0, s, jobs, pages, vlists + 2 * lcap, ctr + 14, ctr + 17,
                        offs, streams, runs, blks);
     hipLaunchKernelGGL(k_char_scan, dim3(n), dim3(256), 0, s, jobs, pages, offs);
-    hipLaunchKernelGGL(k_str_write, dim3(waves), dim3(64), 0, s, jobs, pages, vlists + 2 * lcap, ctr + 14, ctr + 18,
-                       (uint8_t*)c->value_arena.p, offs, streams, runs, blks);
+    hipLaunchKernelGGL(k_str_copy, dim3(c->num_cus * 4), dim3(512), 0, s, jobs, pages, vlists + 2 * lcap, ctr + 14,
+                       ctr + 20, (uint8_t*)c->value_arena.p, offs);
   }
   if (c->timed) hipEventRecord(c->ev[9], s);
   hipLaunchKernelGGL(k_finalize, dim3(n), dim3(256), 0, s, jobs, n, pages);
@@ -605,16 +615,19 @@ int pqg_get_pages(pqg_ctx* c, int job, pqg_page_info* out, int cap) {
 }
 
 // Diagnostic builds (-DPQG_PROFILE): in-kernel phase cycle counters of the
-// values (slots 0-31) and levels (slots 32-63) translation units; read + reset.
+// values (slots 0-31), levels (slots 32-63), strings (64-95) and snappy
+// (96-127) translation units; read + reset.
 int pqg_debug_counters(pqg_ctx* c, uint64_t* out, int cap) {
   if (!c || !out) return PQG_ERR_INVALID_ARG;
 #ifdef PQG_PROFILE
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
-  unsigned long long a[64], b[64];
-  if (pqg::prof_read_values(a) || pqg::prof_read_levels(b)) return PQG_ERR_HIP;
+  unsigned long long a[64], b[64], c3[64], d4[64];
+  if (pqg::prof_read_values(a) || pqg::prof_read_levels(b) || pqg::prof_read_strings(c3) ||
+      pqg::prof_read_snappy(d4))
+    return PQG_ERR_HIP;
   int k = 0;
-  for (; k < 64 && k < cap; k++) out[k] = k < 32 ? a[k] : b[k - 32];
+  for (; k < 128 && k < cap; k++) out[k] = k < 32 ? a[k] : k < 64 ? b[k - 32] : k < 96 ? c3[k - 64] : d4[k - 96];
   return k;
 #else
   return 0;

@@ -11,22 +11,23 @@
 // int64 offsets[num_values + 1] (offsets[0] = 0, offsets[i + 1] = end of
 // value i) — Arrow's large-binary layout.
 //
-//   K7a k_str_dict   one wave per chunk with a byte-array dictionary: walks the
-//                    dictionary page's length chain into the record-start table
-//                    doffs[count + 1], then publishes the dictionary
-//   K7b k_str_count  one wave per byte-array data page: PLAIN pages walk the
-//                    length chain (page-relative value ends, written into the
-//                    chunk's offsets); dictionary pages sum the entry lengths
-//                    of their keys.  -> page.chars
+//   K7a k_str_dict   one block per chunk with a byte-array dictionary: the
+//                    dictionary page's records -> record starts doffs[count + 1],
+//                    then the dictionary is published
+//   K7b k_str_plain  one block per PLAIN byte-array data page: the length chain
+//                    -> page-relative value ends, written into the chunk's
+//                    offsets; page.chars
+//       k_str_count  one wave per dictionary-encoded byte-array page: the sum
+//                    of its keys' entry lengths -> page.chars; the keys are
+//                    parked in the value's offsets slot
 //   K7c k_char_scan  one block per chunk: exclusive scan of page.chars
-//   K7d k_str_write  one wave per byte-array data page: final offsets + chars
+//   K7d k_str_copy   one block per byte-array data page: final offsets + chars
+//                    (copied from the page records, or gathered from the
+//                    dictionary)
 //
-// The length chain is the one serial dependency of the format.  It is walked
-// by the scalar unit over a 1 KiB window held in the wave's VGPRs (64 lanes x 4
-// dwords): a hop is two v_readlane of the dwords under the position, an
-// alignbit and the bounds checks, all wave-uniform, so no LDS round trip sits
-// on the chain.  64 consecutive value ends are collected one per lane and
-// stored by one coalesced wave store.
+// The length chain is the one serial dependency of the format; K7a/K7b cut it
+// into segments walked in parallel from guessed starts and verified in order
+// (block_walk below).
 #include <hip/hip_runtime.h>
 
 #include "pqg_common.h"
@@ -35,115 +36,312 @@
 
 namespace pqg {
 
-// 1 KiB of a byte stream in VGPRs: window dword k lives in d[k >> 6] of lane k & 63.
-struct RegWindow {
-  gcu8 p;        // stream start
-  int64_t n;     // stream bytes
-  int64_t base;  // stream offset of window byte 0 (4-byte aligned address)
-  uint32_t d[4];
+#ifdef PQG_PROFILE
+// host reader of this translation unit's phase counters (see pqg_debug_counters)
+int prof_read_strings(unsigned long long* out) {
+  unsigned long long z[64] = {0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pqg_prof), sizeof(z)) != hipSuccess) return -1;
+  hipMemcpyToSymbol(HIP_SYMBOL(pqg_prof), z, sizeof(z));
+  return 0;
+}
+#define PQG_ACC0(slot, v) do { if (threadIdx.x == 0) atomicAdd(&pqg_prof[slot], (unsigned long long)(v)); } while (0)
+#else
+#define PQG_ACC0(slot, v) do { } while (0)
+#endif
 
-  __device__ __forceinline__ void init(gcu8 p_, int64_t n_) {
-    p = p_;
-    n = n_;
-    base = kFarAway;
-  }
-  __device__ void fill(int64_t at) {
-    const uintptr_t a = (uintptr_t)(p + at);
-    base = at - (int64_t)(a & 3);
-    const int l = lane_id();
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int64_t off = base + 4 * (int64_t)(j * 64 + l);
-      // the dword holds a stream byte < n: it lies in the stream's allocation
-      d[j] = (off + 4 > 0 && off < n) ? *(const PQG_G uint32_t*)(p + off) : 0u;
-    }
-  }
-  __device__ __forceinline__ uint32_t dword(uint32_t k) {
-    const uint32_t j = k >> 6;
-    const uint32_t v = j == 0 ? d[0] : j == 1 ? d[1] : j == 2 ? d[2] : d[3];
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(k & 63));
-  }
-  // u32 at stream offset pos (caller checked pos + 4 <= n)
-  __device__ __forceinline__ uint32_t u32(int64_t pos) {
-    int64_t off = pos - base;
-    if (off < 0 || off + 8 > 1024) {
-      fill(pos);
-      off = pos - base;
-    }
-    const uint32_t k = (uint32_t)off >> 2, sh = ((uint32_t)off & 3) * 8;
-    const uint32_t lo = dword(k), hi = dword(k + 1);
-    return __builtin_amdgcn_alignbit(hi, lo, sh);
-  }
-};
+// ---------------------------------------------------------------------------
+// Block-parallel length-chain walk (PLAIN byte arrays and byte-array
+// dictionary pages).
+//
+// The chain 0 -> 4 + len(0) -> ... is serial, but it is walked in parallel:
+// the byte range is cut into kWalkT segments, and thread t walks the records
+// that start in segment t, from the first position p of the segment whose
+// chain looks valid for three records (u32 length >= 0 and inside the
+// stream).  A walk is only as good as its start; thread 0 then checks, in
+// order, that each segment's start is the position where the true chain
+// (from byte 0) enters the segment — the exit of the previous segment's walk —
+// and re-walks a segment itself when it is not.  The result is exactly the
+// serial chain whatever the data; the guess only decides how much is re-walked
+// (for text-like records: nothing).  A second pass walks every segment again
+// from its verified start and writes the outputs at their record index.
+//
+// Each thread reads through a 64-byte register window (4 aligned granules):
+// every segment walk is a chain of dependent loads, so the window turns a
+// load per record into a load per ~64 bytes.
+// ---------------------------------------------------------------------------
+constexpr int kWalkT = 512;
 
-// byteArrayPlainDecoder.next for values [0, count): a failing value ends the
-// walk with its status.  `sink(i, pos_after, chars_after)` sees every value.
-template <class F>
-__device__ __forceinline__ int walk_lengths(RegWindow& win, int64_t count, int64_t* consumed, int64_t* chars, F&& sink) {
-  int64_t pos = 0, cum = 0;
-  int st = kOK;
-  const int64_t n = win.n;
-  for (int64_t i = 0; i < count; i++) {
-    if (n - pos < 4) { st = kEOF; break; }
-    const int32_t l = (int32_t)win.u32(pos);
-    if (l < 0) { st = kBYTE_ARRAY; break; }
-    if (n - pos - 4 < (int64_t)l) { st = kEOF; break; }
-    pos += 4 + (int64_t)l;
-    cum += l;
-    sink(i, pos, cum);
-  }
-  *consumed = pos;
-  *chars = cum;
-  return st;
+__device__ __forceinline__ uint32_t pick4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+  return (k & 2) ? ((k & 1) ? d : c) : ((k & 1) ? b : a);
 }
 
-// Collects one int64 per value in lane (i & 63) and stores each full batch of 64.
-struct LaneBatch {
-  PQG_G int64_t* out;
-  uint32_t lo, hi;
-  __device__ __forceinline__ void put(int64_t i, int64_t v) {
-    const int l = (int)(i & 63);
-    const bool mine = lane_id() == l;  // v_cmp + two v_cndmask: the value lands in lane l
-    lo = mine ? (uint32_t)v : lo;
-    hi = mine ? (uint32_t)((uint64_t)v >> 32) : hi;
-    if (l == 63) flush(i - 63, 64);
+// Walk records from `pos` while pos < stop and fewer than `limit` records are
+// done.  Returns the records walked; *end = the position after them, *fail = 1
+// when the record at *end is not valid (length negative or past n, or fewer
+// than 4 bytes left).  sink(k, pos_after) sees record k of the walk.
+template <class F>
+__device__ __forceinline__ uint32_t seg_walk(gcu8 p, uint32_t n, uint32_t pos, uint32_t stop, uint32_t limit,
+                                             uint32_t* end, int* fail, F&& sink) {
+  uintptr_t wb = 0;
+  uint4 g0 = make_uint4(0, 0, 0, 0), g1 = g0, g2 = g0, g3 = g0;
+  const uintptr_t pend = (uintptr_t)(p + n);
+  uint32_t k = 0;
+  *fail = 0;
+  while (pos < stop && k < limit) {
+    if (n - pos < 4) { *fail = 1; break; }
+    const uintptr_t a = (uintptr_t)(p + pos);
+    if (a < wb || a + 4 > wb + 64) {
+      wb = a & ~(uintptr_t)15;
+      // four loads issued together, unconditionally (a guarded load would be
+      // waited for at its branch join): granules past the stream's last one
+      // re-read that one, their bytes are never used
+      const uintptr_t lastg = (pend - 1) & ~(uintptr_t)15;
+      g0 = ldg16(wb);
+      g1 = ldg16(wb + 16 < lastg ? wb + 16 : lastg);
+      g2 = ldg16(wb + 32 < lastg ? wb + 32 : lastg);
+      g3 = ldg16(wb + 48 < lastg ? wb + 48 : lastg);
+    }
+    const uint32_t off = (uint32_t)(a - wb), d = off >> 2, e = d + 1 < 16 ? d + 1 : 15;
+    const uint32_t lo = pick4(pick4(g0.x, g0.y, g0.z, g0.w, d), pick4(g1.x, g1.y, g1.z, g1.w, d),
+                              pick4(g2.x, g2.y, g2.z, g2.w, d), pick4(g3.x, g3.y, g3.z, g3.w, d), d >> 2);
+    const uint32_t hi = pick4(pick4(g0.x, g0.y, g0.z, g0.w, e), pick4(g1.x, g1.y, g1.z, g1.w, e),
+                              pick4(g2.x, g2.y, g2.z, g2.w, e), pick4(g3.x, g3.y, g3.z, g3.w, e), e >> 2);
+    const uint32_t l = __builtin_amdgcn_alignbit(hi, lo, (off & 3) * 8);
+    if ((int32_t)l < 0 || n - pos - 4 < l) { *fail = 1; break; }
+    pos += 4 + l;
+    sink(k, pos);
+    k++;
   }
-  __device__ __forceinline__ void flush(int64_t i0, int cnt) {
-    const int lane = lane_id();
-    if (lane < cnt) stg8((uintptr_t)(out + i0 + lane), lo, hi);
-  }
+  *end = pos;
+  return k;
+}
+
+struct BlockWalkShared {
+  uint32_t start[kWalkT];  // pass A: first guessed start (0xffffffff: none); pass B: verified start
+  uint32_t exit_[kWalkT];  // position after the segment's records
+  uint32_t cnt[kWalkT];    // records walked
+  uint32_t start2[kWalkT], exit2[kWalkT], cnt2[kWalkT];  // the second guess
+  uint32_t base[kWalkT];   // pass B: index of the segment's first record (0xffffffff: segment unused)
+  uint8_t fail[kWalkT], fail2[kWalkT];
+  uint32_t last_end;       // end of record count-1
+  int status;
 };
 
+// byteArrayPlainDecoder.next for records [0, count) of [p, p+n), the whole
+// block.  mode 0 (data page): out[i] = char end of value i = end(i) - 4 (i + 1);
+// mode 1 (dictionary page): out[i] = end(i), the next record's start.
+// Returns the status (all threads); *chars = sum of the lengths.
+__device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out, int mode, int64_t* chars,
+                          BlockWalkShared& sh) {
+  const int t = threadIdx.x;
+  const uint32_t L = ((n + kWalkT - 1) / kWalkT + 63) & ~63u;  // segment bytes (>= 64)
+  const uint32_t lo = (uint32_t)t * L < n ? (uint32_t)t * L : n;
+  const uint32_t hi = lo + L < n ? lo + L : n;
+  const uint32_t kNone = 0xffffffffu;
+  auto nop = [](uint32_t, uint32_t) {};
+  PQG_T(tp0);
+  // ---- pass A: guess two starts, walk the segment from each
+  // (a false start is typically the byte before a record — [c, len, 0, 0] reads
+  // as a short length — so the next candidate is usually the true record)
+  if (count > 0) {
+    uint32_t st = kNone, st2 = kNone;
+    if (t == 0) {
+      st = 0;
+    } else {
+      // positions whose length chain is valid for three records; a candidate
+      // is first screened on its own length (one 64-byte window load per 60
+      // positions), the deeper check walks from it
+      uintptr_t wb = 0;
+      uint4 g0 = make_uint4(0, 0, 0, 0), g1 = g0, g2 = g0, g3 = g0;
+      const uintptr_t pend = (uintptr_t)(p + n), lastg = (pend - 1) & ~(uintptr_t)15;
+      for (uint32_t q = lo; q < hi && n - q >= 4; q++) {
+        if (st != kNone && q > st + 64) break;
+        const uintptr_t a = (uintptr_t)(p + q);
+        if (a + 4 > wb + 64) {
+          wb = a & ~(uintptr_t)15;
+          g0 = ldg16(wb);
+          g1 = ldg16(wb + 16 < lastg ? wb + 16 : lastg);
+          g2 = ldg16(wb + 32 < lastg ? wb + 32 : lastg);
+          g3 = ldg16(wb + 48 < lastg ? wb + 48 : lastg);
+        }
+        const uint32_t off = (uint32_t)(a - wb), d = off >> 2, e1 = d + 1 < 16 ? d + 1 : 15;
+        const uint32_t w0 = pick4(pick4(g0.x, g0.y, g0.z, g0.w, d), pick4(g1.x, g1.y, g1.z, g1.w, d),
+                                  pick4(g2.x, g2.y, g2.z, g2.w, d), pick4(g3.x, g3.y, g3.z, g3.w, d), d >> 2);
+        const uint32_t w1 = pick4(pick4(g0.x, g0.y, g0.z, g0.w, e1), pick4(g1.x, g1.y, g1.z, g1.w, e1),
+                                  pick4(g2.x, g2.y, g2.z, g2.w, e1), pick4(g3.x, g3.y, g3.z, g3.w, e1), e1 >> 2);
+        const uint32_t l = __builtin_amdgcn_alignbit(w1, w0, (off & 3) * 8);
+        if ((int32_t)l < 0 || n - q - 4 < l) continue;
+        uint32_t e;
+        int f;
+        const uint32_t k = seg_walk(p, n, q, n, 3, &e, &f, nop);
+        if (k == 3 || (f && e == n)) {
+          if (st == kNone) {
+            st = q;
+          } else {
+            st2 = q;
+            break;
+          }
+        }
+      }
+    }
+    sh.start[t] = st;
+    sh.start2[t] = st2;
+    sh.fail[t] = sh.fail2[t] = 0;
+    sh.cnt[t] = sh.cnt2[t] = 0;
+    sh.exit_[t] = st;
+    sh.exit2[t] = st2;
+    uint32_t e;
+    int f;
+    if (st != kNone && st < hi) {
+      sh.cnt[t] = seg_walk(p, n, st, hi, 0xffffffffu, &e, &f, nop);
+      sh.exit_[t] = e;
+      sh.fail[t] = (uint8_t)f;
+    }
+    if (st2 != kNone && st2 < hi) {
+      sh.cnt2[t] = seg_walk(p, n, st2, hi, 0xffffffffu, &e, &f, nop);
+      sh.exit2[t] = e;
+      sh.fail2[t] = (uint8_t)f;
+    }
+  }
+  __syncthreads();
+  PQG_T(tp1);
+  // ---- thread 0: follow the true chain through the segments
+  if (t == 0) {
+    uint32_t redo = 0, redo_k = 0;
+    (void)redo;
+    (void)redo_k;
+    for (int s = 0; s < kWalkT; s++) sh.base[s] = kNone;
+    uint32_t cur = 0, idx = 0;
+    int status = kOK;
+    bool failed = false;
+    for (int s = 0; s < kWalkT && idx < count; s++) {
+      const uint32_t slo = (uint32_t)s * L < n ? (uint32_t)s * L : n;
+      const uint32_t shi = slo + L < n ? slo + L : n;
+      if (shi <= slo) break;     // past the end of the stream
+      if (cur >= shi) continue;  // a record spans the whole segment
+      uint32_t k, e;
+      int f;
+      if (sh.start[s] == cur) {  // a guess was right: take the segment's walk
+        k = sh.cnt[s];
+        e = sh.exit_[s];
+        f = sh.fail[s];
+      } else if (sh.start2[s] == cur) {
+        k = sh.cnt2[s];
+        e = sh.exit2[s];
+        f = sh.fail2[s];
+      } else {
+        k = seg_walk(p, n, cur, shi, 0xffffffffu, &e, &f, nop);
+        redo++;
+        redo_k += k;
+      }
+      sh.start[s] = cur;
+      sh.base[s] = idx;
+      idx += k;
+      cur = e;
+      if (f) {
+        failed = true;
+        break;
+      }
+    }
+    if (idx < count) {
+      // record `idx` at `cur` fails: fewer than 4 bytes (EOF), a negative
+      // length, or fewer bytes than its length (EOF)
+      status = kEOF;
+      if (failed && n - cur >= 4) {
+        const uint32_t l = (uint32_t)p[cur] | (uint32_t)p[cur + 1] << 8 | (uint32_t)p[cur + 2] << 16 |
+                           (uint32_t)p[cur + 3] << 24;
+        if ((int32_t)l < 0) status = kBYTE_ARRAY;
+      }
+    }
+    sh.status = status;
+    sh.last_end = 0;
+    PQG_ACC0(20, redo);
+    PQG_ACC0(21, redo_k);
+  }
+  __syncthreads();
+  PQG_T(tp2);
+  const int status = sh.status;
+  if (status != kOK) return status;
+  // ---- pass B: outputs from the verified starts
+  if (count > 0 && sh.base[t] != kNone && sh.base[t] < count) {
+    const uint32_t b = sh.base[t];
+    uint32_t e;
+    int f;
+    seg_walk(p, n, sh.start[t], hi, count - b, &e, &f,
+             [&](uint32_t k, uint32_t pos) {
+               const uint32_t i = b + k;
+               out[i] = mode ? (int64_t)pos : (int64_t)pos - 4 * ((int64_t)i + 1);
+               if (i == count - 1) sh.last_end = pos;
+             });
+  }
+  __syncthreads();
+  PQG_T(tp3);
+#ifdef PQG_PROFILE
+  PQG_ACC0(16, tp1 - tp0);
+  PQG_ACC0(17, tp2 - tp1);
+  PQG_ACC0(18, tp3 - tp2);
+  PQG_ACC0(19, 1);
+#endif
+  *chars = count ? (int64_t)sh.last_end - 4 * (int64_t)count : 0;
+  return kOK;
+}
+
 // ---- K7a ---------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_str_dict(JobDev* jobs, PageDev* pages, int64_t* doffs_arena) {
+__global__ void __launch_bounds__(kWalkT) k_str_dict(JobDev* jobs, PageDev* pages, int64_t* doffs_arena) {
+  __shared__ BlockWalkShared sh;
   JobDev& job = jobs[blockIdx.x];
   if (job.status == kCAPACITY || !(job.flags & 2) || job.dict_page < 0) return;
   PageDev& dp = pages[job.page_base + job.dict_page];
   if (dp.read_status != kOK) return;
   const int64_t cnt = dp.num_values;
   PQG_G int64_t* doffs = gmut(doffs_arena) + job.doffs_base;
-  RegWindow win;
-  win.init(gconst(job.dict_data), job.dict_len);
-  LaneBatch lb{doffs + 1, 0u, 0u};
-  int64_t used, chars;
-  const int st = walk_lengths(win, cnt, &used, &chars, [&](int64_t i, int64_t pos, int64_t) { lb.put(i, pos); });
-  const int64_t done = st == kOK ? cnt : 0;
-  if (st == kOK) lb.flush(cnt & ~(int64_t)63, (int)(cnt & 63));
-  __builtin_amdgcn_wave_barrier();
-  if (lane_id() == 0) {
+  int64_t chars;
+  const int st = block_walk(gconst(job.dict_data), (uint32_t)job.dict_len, (uint32_t)cnt, doffs + 1, 1, &chars, sh);
+  if (threadIdx.x == 0) {
     if (st == kOK) {
       doffs[0] = 0;
       job.dict_offs = (const int64_t*)doffs;
-      job.dict_count = done;
+      job.dict_count = cnt;
     } else {
       dp.read_status = st;  // dictPageReader.read: any error is fatal (page_dict.go:50-56)
     }
   }
 }
 
+// ---- K7b (PLAIN) -------------------------------------------------------------
+__global__ void __launch_bounds__(kWalkT) k_str_plain(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+                                                      int* queue, int64_t* offs_arena) {
+  __shared__ BlockWalkShared sh;
+  __shared__ int s_t;
+  for (;;) {
+    if (threadIdx.x == 0) s_t = atomicAdd(queue, 1);
+    __syncthreads();
+    const int t = s_t;
+    __syncthreads();
+    if (t >= *total) return;
+    const int pidx = list[t];
+    const PageDev& pg = pages[pidx];
+    if (pg.read_status != kOK || pg.decode_status != kOK || (pg.page_type != 0 && pg.page_type != 3) ||
+        pg.encoding != 0 || pg.not_null == 0)
+      continue;
+    const JobDev& job = jobs[pg.job];
+    if (job.status == kCAPACITY) continue;
+    int64_t chars;
+    const int de = block_walk(gconst(pg.val), (uint32_t)pg.val_n, (uint32_t)pg.not_null,
+                              gmut(offs_arena) + job.offs_base + pg.value_offset + 1, 0, &chars, sh);
+    if (threadIdx.x == 0) {
+      pages[pidx].chars = de == kOK ? chars : 0;
+      if (de != kOK) pages[pidx].decode_status = de;
+    }
+  }
+}
+
 // ---- dictionary sinks (type_dict.go:39-59 over variable-length entries) ------
+// Sums the entry lengths of the keys and parks each key in its value's
+// offsets slot (k_str_copy turns it into the value's end).
 struct StrDictCount {
   const PQG_G int64_t* doffs;
+  PQG_G int64_t* keys;  // chunk offsets + value_offset + 1
   int64_t count;
   int64_t bad;   // first value index with an invalid key
   int64_t sum;   // lane's chars
@@ -153,6 +351,7 @@ struct StrDictCount {
     for (int b = 0; b < kGroup; b++)
       for (int q = 0; q < cnt[b]; q++) {
         const uint32_t key = v[b][q];
+        keys[i0[b] + q] = key;
         if ((int64_t)key < count) sum += doffs[key + 1] - doffs[key] - 4;
         else if ((int64_t)(i0[b] + q) < bad) bad = (int64_t)(i0[b] + q);
       }
@@ -180,44 +379,6 @@ __device__ __forceinline__ void copy_bytes(gu8 dst, gcu8 src, int64_t len) {
   }
   for (; k < len; k++) dst[k] = src[k];
 }
-
-struct StrDictWrite {
-  gu8 chars;                 // chunk chars + the page's char offset
-  PQG_G int64_t* ends;       // chunk offsets + value_offset + 1
-  int64_t base;              // the page's char offset in the chunk
-  gcu8 dict;                 // dictionary page block
-  const PQG_G int64_t* doffs;
-  int64_t count;
-  int64_t carry;             // page chars written before this group (wave-uniform)
-  __device__ __forceinline__ void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup],
-                                        const int (&cnt)[kGroup]) {
-#pragma unroll
-    for (int b = 0; b < kGroup; b++) {
-      int64_t src[8];
-      int32_t len[8];
-      int64_t s = 0;
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        len[q] = 0;
-        src[q] = 0;
-        if (q < cnt[b] && (int64_t)v[b][q] < count) {
-          const int64_t a = doffs[v[b][q]];
-          len[q] = (int32_t)(doffs[v[b][q] + 1] - a - 4);
-          src[q] = a + 4;
-        }
-        s += len[q];
-      }
-      int64_t tot;
-      int64_t pos = carry + wave_excl_scan_i64(s, &tot);
-      for (int q = 0; q < cnt[b]; q++) {
-        copy_bytes(chars + pos, dict + src[q], len[q]);
-        pos += len[q];
-        ends[i0[b] + q] = base + pos;
-      }
-      carry += tot;
-    }
-  }
-};
 
 // ---- K7b ---------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_str_count(JobDev* jobs, PageDev* pages, const int* list, const int* total,
@@ -251,23 +412,22 @@ __global__ void __launch_bounds__(64) k_str_count(JobDev* jobs, PageDev* pages, 
     int de = kOK;
     int64_t chars = 0;
     if (enc == 0) {
-      RegWindow win;
-      win.init(val, vn);
-      LaneBatch lb{gmut(offs_arena) + job.offs_base + pg.value_offset + 1, 0u, 0u};
-      int64_t used;
-      de = walk_lengths(win, nn, &used, &chars, [&](int64_t i, int64_t, int64_t cum) { lb.put(i, cum); });
-      if (de == kOK) lb.flush(nn & ~(int64_t)63, (int)(nn & 63));
+      continue;  // PLAIN: k_str_plain
     } else if (enc == 8) {
       const int64_t dcount = job.dict_offs ? job.dict_count : 0;
       const int dw = pg.dict_width;
+      PQG_G int64_t* keys = gmut(offs_arena) + job.offs_base + pg.value_offset + 1;
       if (dw == 0) {
         // zero-width indices: key 0 forever (hybrid_decoder.go:84-86)
         if (dcount < 1) de = kDICT_INDEX;
-        else chars = nn * (gconst(job.dict_offs)[1] - 4);
+        else {
+          chars = nn * (gconst(job.dict_offs)[1] - 4);
+          for (int64_t i = lane; i < nn; i += 64) keys[i] = 0;
+        }
       } else {
         const HStream S = streams[pg.hs_val];
         const int serr = (S.status != kOK && S.produced < nn) ? S.status : kOK;
-        StrDictCount sk{gconst(job.dict_offs ? job.dict_offs : (const int64_t*)offs_arena), dcount, nn, 0};
+        StrDictCount sk{gconst(job.dict_offs ? job.dict_offs : (const int64_t*)offs_arena), keys, dcount, nn, 0};
         hybrid_expand(S, runs, blks, nn, sh, sk);
         const int64_t bad = wave_min(sk.bad);
         chars = wave_sum(sk.sum);
@@ -311,55 +471,74 @@ __global__ void __launch_bounds__(256) k_char_scan(JobDev* jobs, PageDev* pages,
   }
 }
 
-// ---- K7d ---------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_str_write(JobDev* jobs, PageDev* pages, const int* list, const int* total,
-                                                  int* queue, uint8_t* value_arena, int64_t* offs_arena,
-                                                  const HStream* streams, const RunEnt* runs, const BlockDesc* blks) {
-  __shared__ __attribute__((aligned(16))) ExpandShared sh;
-  const int lane = lane_id();
+}  // namespace pqg
+
+namespace pqg {
+
+// ---- K7d -----------------------------------------------------------------------
+// One block per byte-array data page, one value per thread.  PLAIN: value i's
+// chars [e(i-1), e(i)) come from its record at e(i-1) + 4 (i + 1) of the page's
+// value section (k_str_plain left the page-relative ends in the offsets).
+// Dictionary: the slot holds the key (k_str_count); the value is dictionary
+// entry `key`, and its start is a block scan of the entry lengths.  The ends
+// become chunk offsets.  512 independent copies per block keep many loads in
+// flight.
+__global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+                                                  int* queue, uint8_t* value_arena, int64_t* offs_arena) {
+  __shared__ int s_t;
+  __shared__ int64_t s_prev;  // page-relative end of the value before the round
+  __shared__ int64_t part[9];
   for (;;) {
-    const int t = queue_next(queue);
+    if (threadIdx.x == 0) {
+      s_t = atomicAdd(queue, 1);
+      s_prev = 0;
+    }
+    __syncthreads();
+    const int t = s_t;
+    __syncthreads();
     if (t >= *total) return;
-    const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
-    const PageDev pg = pages[pidx];
-    if (pg.read_status != kOK || pg.decode_status != kOK || (pg.page_type != 0 && pg.page_type != 3)) continue;
-    const JobDev job = jobs[pg.job];
+    const int pidx = list[t];
+    const PageDev& pg = pages[pidx];
+    if (pg.read_status != kOK || pg.decode_status != kOK || (pg.page_type != 0 && pg.page_type != 3) ||
+        pg.not_null == 0)
+      continue;
+    const JobDev& job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
-    const int64_t nn = pg.not_null;
-    if (nn == 0) continue;
-    const gu8 chars = gmut(value_arena) + job.value_base + pg.char_offset;
+    const int64_t nn = pg.not_null, base = pg.char_offset;
+    const gu8 chars = gmut(value_arena) + job.value_base + base;
     PQG_G int64_t* ends = gmut(offs_arena) + job.offs_base + pg.value_offset + 1;
-    const int64_t base = pg.char_offset;
-    if (pg.encoding == 0) {
-      // PLAIN: value i's record starts at (its chars' start) + 4 (i + 1) - 4
-      const gcu8 val = gconst(pg.val);
-      int64_t prev = 0;  // page-relative end of the value before the batch
-      for (int64_t i0 = 0; i0 < nn; i0 += 64) {
-        const int64_t i = i0 + lane;
-        int64_t e = 0;
-        if (i < nn) e = ends[i];
-        int64_t s = __shfl_up(e, 1, 64);
-        if (lane == 0) s = prev;
+    const bool dict = pg.encoding == 8;
+    const gcu8 src = dict ? gconst(job.dict_data) : gconst(pg.val);
+    const PQG_G int64_t* doffs = gconst(job.dict_offs);
+    for (int64_t i0 = 0; i0 < nn; i0 += 512) {
+      const int64_t i = i0 + threadIdx.x;
+      int64_t e = 0, s0 = 0, from = 0;
+      if (dict) {
+        int64_t len = 0;
         if (i < nn) {
-          copy_bytes(chars + s, val + s + 4 * (i + 1), e - s);
-          ends[i] = base + e;
+          const int64_t key = ends[i];
+          from = doffs[key] + 4;
+          len = doffs[key + 1] - from;
         }
-        prev = __shfl(e, 63, 64);
-      }
-    } else {
-      const gcu8 dict = gconst(job.dict_data);
-      const PQG_G int64_t* doffs = gconst(job.dict_offs);
-      if (pg.dict_width == 0) {
-        const int64_t l = doffs[1] - 4;
-        for (int64_t i = lane; i < nn; i += 64) {
-          copy_bytes(chars + i * l, dict + 4, l);
-          ends[i] = base + (i + 1) * l;
-        }
+        int64_t tot;
+        const int64_t prev = s_prev;  // read before the scan's barriers: thread 0 moves it after
+        s0 = prev + block_excl_scan<512>(len, &tot, part);
+        e = s0 + len;
+        if (threadIdx.x == 0) s_prev += tot;  // after the scan's last barrier
       } else {
-        const HStream S = streams[pg.hs_val];
-        StrDictWrite sk{chars, ends, base, dict, doffs, job.dict_count, 0};
-        hybrid_expand(S, runs, blks, nn, sh, sk);
+        if (i < nn) {
+          e = ends[i];
+          s0 = threadIdx.x ? ends[i - 1] : s_prev;
+          from = s0 + 4 * (i + 1);
+        }
+        __syncthreads();  // every end of the round is read before any is rewritten
+        if (i == (i0 + 512 < nn ? i0 + 511 : nn - 1)) s_prev = e;
       }
+      if (i < nn) {
+        copy_bytes(chars + s0, src + from, e - s0);
+        ends[i] = base + e;
+      }
+      __syncthreads();
     }
   }
 }

@@ -401,29 +401,17 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
         int64_t full = vn / 12, rem = vn % 12;
         if (nn > full + (rem > 0 ? 1 : 0)) de = kEOF;
         else {
+          // a partial final value is left nil (Q8): its bytes are zero
+          const int64_t whole = nn < full ? nn : full;
           if (nn == full + 1 && rem > 0 && lane == 0) pages[pidx].flags |= 1;
-          for (int64_t i = lane; i < nn * 12; i += 64) out[i] = (i < full * 12) ? val[i] : 0;
+          wave_copy(out, val, whole * 12);
+          if (whole < nn && lane < 12) out[whole * 12 + lane] = 0;
         }
-      } else if (w > 0 && (w & 3) != 0) {  // FLBA of odd length: byte copy
+      } else if (w > 0) {  // INT32 / INT64 / FLOAT / DOUBLE / FLBA: little-endian bit copies
         if (nn * w > vn) de = kEOF;
-        else
-          for (int64_t i = lane; i < nn * w; i += 64) out[i] = val[i];
-      } else if (w > 0) {
-        if (nn * w > vn) de = kEOF;
-        else {
-          int64_t nb = nn * w;
-          // 16-byte destination chunks; source may be unaligned
-          for (int64_t i = (int64_t)lane * 4; i < nb; i += 256) {
-            if (i + 4 <= nb) {
-              uint64_t x = load_u64_masked(val, readable, i, vn);
-              *(PQG_G uint32_t*)(out + i) = (uint32_t)x;
-            } else {
-              for (int64_t b = i; b < nb; b++) out[b] = val[b];
-            }
-          }
-        }
+        else wave_copy(out, val, nn * w);
       } else {
-        de = kUNSUPPORTED;  // PLAIN byte arrays: not in this build yet
+        de = kUNSUPPORTED;  // variable length: pqg_strings.hip
       }
     } else if (enc == 8) {
       const gcu8 dict = gconst(job.dict_data);

@@ -522,3 +522,34 @@ def test_c5_single_page_chunks(dec):
     """parquet-go's own writer puts one data page in each chunk (chunk_writer.go:237-246)."""
     data, _ = W.config_c5(row_groups=(5,), rows_per_rg=30_000, rows_per_page=30_000)
     P.compare_file(data, dec)
+
+
+def test_byte_array_chain_guesses_wrong(dec):
+    """PLAIN byte arrays whose bytes look like length prefixes everywhere (zero
+    bytes, embedded u32 lengths): the segment walks start at wrong guesses and
+    the in-order check must re-walk them; big pages span hundreds of segments."""
+    rng = np.random.default_rng(21)
+    n = 60_000
+    for kind in ("zeros", "fake_prefix", "mixed"):
+        lens = rng.integers(0, 24, size=n)
+        offs = np.r_[0, np.cumsum(lens)].astype(np.int64)
+        if kind == "zeros":
+            chars = np.zeros(int(offs[-1]), np.uint8)
+        elif kind == "fake_prefix":
+            pat = np.frombuffer(np.array([4, 8, 0, 3], dtype=np.uint32).tobytes(), np.uint8)
+            chars = np.resize(pat, int(offs[-1]))
+        else:
+            chars = rng.integers(0, 3, size=int(offs[-1])).astype(np.uint8)
+        for rpp in (n, 7000):
+            col = W.Column("s", W.BYTE_ARRAY, chars, offsets=offs, rows_per_page=rpp)
+            P.compare_file(W.write_file([col], n), dec)
+    # a string dictionary of such entries, then a corrupt tail inside a big page
+    col = W.Column("s", W.BYTE_ARRAY, np.zeros(int(offs[-1]), np.uint8), offsets=offs, rows_per_page=n)
+    data = bytearray(W.write_file([col], n))
+    import pqgpu
+    pf = pqgpu.ParquetFile(bytes(data))
+    m = pf.chunk_meta(0, 0)
+    for at, val in ((m.start + m.total_compressed_size - 9, 0xFF), (m.start + m.total_compressed_size // 2, 0x80)):
+        b = bytearray(data)
+        b[at] = val
+        P.compare_file(bytes(b), dec)

@@ -1,8 +1,14 @@
-"""Multi-rank path on CPU (gloo, world_size 2): row-group shards decoded
-independently per rank reproduce the single-process decode, with no
-collective other than the timing reduction.
-The per-rank decoder here is the oracle (no GPU in this container); on the
-GPU box bench.py runs the same sharding with libpqgpu per rank."""
+"""Multi-rank path: row-group shards decoded
+independently per rank reproduce the single-process decode, with no collective
+other than the barrier and the timing reduction.
+
+The ranks build their work exactly as bench.py does (bench.gen_workload:
+pqgpu.shard.row_groups_for_rank over the C5 row groups, each generated from
+its global index).  On CPU (gloo, world size 2) each rank decodes its shard
+with the oracle; the GPU variant (-m gpu) runs both ranks on cuda:0 and
+decodes through pqg_decode_chunks, as bench.py does per GPU."""
+import argparse
+import hashlib
 import os
 import socket
 
@@ -11,6 +17,8 @@ import pytest
 import torch.multiprocessing as mp
 
 from pqgpu import shard
+
+ROWS_PER_RG = 3000
 
 
 def _free_port():
@@ -21,45 +29,101 @@ def _free_port():
     return p
 
 
-def _file():
-    from gen import pqwrite as W
-    rng = np.random.default_rng(7)
-    rows = 6 * 3000
-    defs = (rng.random(rows) >= 0.1).astype(np.uint8)
-    vals = rng.integers(0, 1 << 10, size=int(defs.sum())).astype(np.int32)
-    c1 = W.Column("a", W.INT32, vals, repetition=W.OPTIONAL, encoding=W.RLE_DICTIONARY, def_levels=defs,
-                  rows_per_page=1000)
-    c2 = W.Column("b", W.INT64, rng.integers(-2**40, 2**40, size=rows), rows_per_page=700)
-    return W.write_file([c1, c2], rows, row_groups=6)
+def _args():
+    return argparse.Namespace(c5_rows_per_rg=ROWS_PER_RG, rows=0, bits="")
 
 
-def _digest(chunk):
-    parts = [np.array([chunk.status, chunk.num_slots, chunk.num_values], dtype=np.int64).tobytes()]
-    for a in (chunk.def_levels, chunk.rep_levels, chunk.values):
-        if a is not None:
-            parts.append(np.ascontiguousarray(a).tobytes())
-    import hashlib
+def _digest(status, slots, nvals, arrays):
+    parts = [np.array([status, slots, nvals], dtype=np.int64).tobytes()]
+    parts += [np.ascontiguousarray(a).tobytes() for a in arrays if a is not None]
     return hashlib.sha256(b"".join(parts)).hexdigest()
 
 
-def _worker(rank, world, port, q):
+def _oracle_digest(job):
+    from oracle import pyoracle as O
+    r = O.decode_chunk(job)
+    return _digest(r.status, r.num_slots, r.num_values, (r.def_levels, r.rep_levels, r.values, r.offsets))
+
+
+def _decode_shard(rank, world, gpu):
+    """This rank's C5 shard, built and decoded the way bench.py builds it:
+    {(global rg, col): digest}."""
+    import bench
+    import pqgpu
+    wl = bench.gen_workload("c5", _args(), rank, world)
+    pf, specs, (_, info) = wl.files[0]
+    rgs = info["row_groups"]
+    assert rgs == list(shard.row_groups_for_rank(8 * world, rank, world))
+    out = {}
+    if gpu:
+        dec = pqgpu.GpuDecoder(0)
+        dev = dec.upload(pf.data)
+        try:
+            res = dec.decode_jobs([pqgpu.device_job(pf, rg, col, dev) for (rg, col) in specs])
+            for i, ((rg, col), r) in enumerate(zip(specs, res)):
+                d = dec.download(r, i)
+                out[(rgs[rg], col)] = _digest(d.status, d.num_slots, d.num_values,
+                                              (d.def_levels, d.rep_levels, d.values, d.offsets))
+        finally:
+            dec.free(dev)
+            dec.close()
+    else:
+        for (rg, col) in specs:
+            out[(rgs[rg], col)] = _oracle_digest(pf.host_job(rg, col)[0])
+    return out
+
+
+def _worker(rank, world, port, q, gpu):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "parquet-go_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        import pqgpu
-        from oracle import pyoracle as O
-        pf = pqgpu.ParquetFile(_file())
-        mine = {}
-        for rg, c, job in shard.shard_jobs(pf, rank, world, make_job=lambda p, r, c: p.host_job(r, c)[0]):
-            mine[(rg, c)] = _digest(O.decode_chunk(job))
+        mine = _decode_shard(rank, world, gpu)
         gathered = [None] * world
-        dist.all_gather_object(gathered, mine)
+        dist.all_gather_object(gathered, mine)  # test-side merge only; bench.py has no data-path collective
         t = shard.max_elapsed(0.5 + rank, dist)
         if rank == 0:
             q.put((gathered, t))
     finally:
         dist.destroy_process_group()
+
+
+def _run_two_ranks(gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, gpu)) for r in range(2)]
+    for p in procs:
+        p.start()
+    gathered, t = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return gathered, t
+
+
+def _check_merge(gathered, world):
+    """Each rank holds exactly its row groups; the union equals the
+    single-process decode of the whole 8*world-row-group file."""
+    import pqgpu
+    from gen import pqwrite as W
+    R = 8 * world
+    merged = {}
+    for r, part in enumerate(gathered):
+        for (rg, c), d in part.items():
+            assert shard.rank_of_row_group(rg, R, world) == r
+            merged[(rg, c)] = d
+    data, _ = W.config_c5(row_groups=range(R), rows_per_rg=ROWS_PER_RG)
+    pf = pqgpu.ParquetFile(data)
+    assert sorted(merged) == [(rg, c) for rg in range(R) for c in range(pf.num_columns)]
+    for rg in range(R):
+        for c in range(pf.num_columns):
+            assert merged[(rg, c)] == _oracle_digest(pf.host_job(rg, c)[0]), (rg, c)
 
 
 def test_partition_covers_all_row_groups():
@@ -75,26 +139,14 @@ def test_partition_covers_all_row_groups():
 
 
 def test_two_rank_gloo_shards_match_single_process():
-    import pqgpu
-    from oracle import pyoracle as O
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    gathered, t = q.get(timeout=240)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    gathered, t = _run_two_ranks(gpu=False)
     assert t == 1.5  # MAX over ranks
-    merged = {}
-    for r, part in enumerate(gathered):
-        for (rg, c), d in part.items():
-            assert shard.rank_of_row_group(rg, 6, 2) == r
-            merged[(rg, c)] = d
-    pf = pqgpu.ParquetFile(_file())
-    assert sorted(merged) == [(rg, c) for rg in range(pf.num_row_groups) for c in range(pf.num_columns)]
-    for rg in range(pf.num_row_groups):
-        for c in range(pf.num_columns):
-            assert merged[(rg, c)] == _digest(O.decode_chunk(pf.host_job(rg, c)[0]))
+    _check_merge(gathered, 2)
+
+
+@pytest.mark.gpu
+def test_two_rank_gpu_shards_match_single_process():
+    """Both ranks on cuda:0, each decoding its shard with libpqgpu."""
+    gathered, t = _run_two_ranks(gpu=True)
+    assert t == 1.5
+    _check_merge(gathered, 2)
