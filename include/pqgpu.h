@@ -128,8 +128,22 @@ typedef struct pqg_chunk_job {
   int64_t num_values_hint;       /* ColumnMetaData.num_values (capacity hint only)     */
   int64_t total_uncompressed_size; /* ColumnMetaData.total_uncompressed_size (hint)     */
   int32_t has_dict_page_offset;  /* ColumnMetaData.DictionaryPageOffset != nil         */
-  int32_t reserved;
+  int32_t quirks;                /* PQG_QUIRK_* mask; libpqgpu decodes spec-correctly
+                                    and rejects a non-zero mask (PQG_ERR_INVALID_ARG):
+                                    quirk reproduction is the oracle's triage mode
+                                    (pqo_decode_column_store)                        */
 } pqg_chunk_job;
+
+/* The reference's caller-side stitching defects (DESIGN.md "Quirk
+ * policy").  Q1: readPageData appends each page's whole numValues-long slice,
+ * numValues - notNull trailing nils included (chunk_reader.go:394-397).  Q2:
+ * from the second row group on, the dictionary page decodes into the column
+ * store's reused backing array (chunk_reader.go:235, page_dict.go:50-53), which
+ * the first data page's append then overwrites (type_dict.go:72-79). */
+enum {
+  PQG_QUIRK_Q1_PAGE_NILS = 1,
+  PQG_QUIRK_Q2_DICT_ALIAS = 2
+};
 
 /* Decoded column chunk.  Fixed-width physical types (INT32/INT64/INT96/FLOAT/
  * DOUBLE/FLBA>0/BOOLEAN) store values densely, little endian, `value_width`
@@ -199,6 +213,41 @@ int pqg_sync(pqg_ctx* ctx, pqg_chunk_result* results, int n_jobs);
 /* Convenience: async + sync. */
 int pqg_decode_chunks(pqg_ctx* ctx, const pqg_chunk_job* jobs, int n_jobs,
                       pqg_chunk_result* results);
+
+/* ---- page-level and codec-level entries ------------------------------------ */
+
+/* One data page (and optionally its chunk's dictionary page), both DEVICE
+ * pointers to a thrift PageHeader followed by the page body.  Decoding it is
+ * pageReader.read + readValues (interfaces.go:10-17; page_v1.go:27-108,
+ * page_v2.go:26-129, dictionary: page_dict.go:30-64): the result holds that
+ * page's rLevels, dLevels and values[:notNull] (or chars + offsets), the page
+ * table lists the dictionary page (if any) and the data page. */
+typedef struct pqg_page_job {
+  pqg_column_desc col;
+  const uint8_t* page;       /* DEVICE: PageHeader + body of a DATA_PAGE / DATA_PAGE_V2 */
+  int64_t page_len;
+  const uint8_t* dict_page;  /* DEVICE: PageHeader + body of the DICTIONARY_PAGE, or NULL */
+  int64_t dict_page_len;
+} pqg_page_job;
+int pqg_decode_page(pqg_ctx* ctx, const pqg_page_job* job, pqg_chunk_result* result);
+
+/* BlockCompressor.DecompressBlock (compress.go:24-27, 46-48, registered with
+ * RegisterBlockCompressor compress.go:124-135): decompress one HOST block
+ * synchronously on the GPU.  codec SNAPPY (snappy.Decode semantics: decoded
+ * length from the block's varint header, ErrCorrupt -> PQG_ERR_SNAPPY) or
+ * UNCOMPRESSED (a copy); GZIP -> PQG_ERR_UNSUPPORTED.  *out_len is the decoded
+ * length; PQG_ERR_CAPACITY when it exceeds `cap` (nothing written). */
+int pqg_block_decompress(pqg_ctx* ctx, int codec, const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap,
+                         int64_t* out_len);
+
+/* ColumnStore refill (the Go adapter's half of the drop-in): pack `n` levels
+ * (u8, DEVICE) the way packedArray stores them (packed_array.go:34-101): width
+ * bw = bits.Len16(max_level), each group of 8 levels in bw bytes in the
+ * unpack8int32 layout (LSB first, bitbacking32.go), the last group zero padded
+ * (packedArray.flush).  `packed` (DEVICE) receives ceil(n/8) * bw bytes; a
+ * packedArray refill takes the floor(n/8) * bw bytes as `data` and the last
+ * n % 8 levels as its pending buffer. */
+int pqg_pack_levels(pqg_ctx* ctx, const uint8_t* levels, int64_t n, int max_level, uint8_t* packed);
 
 /* After pqg_sync: page table of job `job` (host copy).  Returns pages written
  * or a negative status. */
@@ -340,9 +389,31 @@ int pqo_hybrid_decode(const uint8_t* buf, int64_t len, int width, int64_t count,
 int pqo_snappy_decode(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int64_t* out_len);
 int pqo_delta_decode64(const uint8_t* buf, int64_t len, int64_t count, int64_t* out);
 int pqo_delta_decode32(const uint8_t* buf, int64_t len, int64_t count, int32_t* out);
+/* Reference column-store contents (triage of Q1/Q2; fixed-width columns):
+ * decode the chunks of one column over `n_row_groups` consecutive row groups
+ * the way readRowGroup fills ColumnStore.values (readPageData
+ * chunk_reader.go:380-402), with the quirks in `quirks` reproduced
+ * (Q2 requires Q1, as in the reference).  Per row group: `entries` store
+ * slots, `values` entries x value_width bytes (a nil slot is zeros),
+ * `nil_flags` one byte per entry.  Q2 follows Go 1.13's slice growth
+ * (runtime growslice + malloc size classes) for []interface{}: outside
+ * /root/reference, stated in the oracle, so parity for it is unpinned. */
+typedef struct pqo_store_rg {
+  int32_t status;
+  int32_t value_width;
+  int64_t entries;
+  uint8_t* values;
+  uint8_t* nil_flags;
+} pqo_store_rg;
+int pqo_decode_column_store(const pqg_chunk_job* jobs, int n_row_groups, int quirks, pqo_store_rg* out);
+void pqo_free_store(pqo_store_rg* out, int n_row_groups);
 /* K8 restatements (host pointers): the ColumnStore.get / getData cursor walks */
 int pqo_assemble(pqg_assemble_args* args);
 int pqo_assemble_list(pqg_list_args* args);
+/* packedArray layout of levels (host pointers): see pqg_pack_levels */
+int pqo_pack_levels(const uint8_t* levels, int64_t n, int max_level, uint8_t* packed);
+/* test hook of the Q2 emulation: Go 1.13 malloc size-class rounding */
+int64_t pqo_go_roundupsize(int64_t size);
 
 #ifdef __cplusplus
 }

@@ -18,6 +18,12 @@ from pqgpu import abi  # noqa: E402
 _lib = None
 
 
+class StoreRG(C.Structure):
+    """pqo_store_rg (include/pqgpu.h)."""
+    _fields_ = [("status", C.c_int32), ("value_width", C.c_int32), ("entries", C.c_int64),
+                ("values", C.c_void_p), ("nil_flags", C.c_void_p)]
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -36,6 +42,11 @@ def lib():
         L.pqo_delta_decode32.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_void_p]
         L.pqo_assemble.argtypes = [C.POINTER(abi.AssembleArgs)]
         L.pqo_assemble_list.argtypes = [C.POINTER(abi.ListArgs)]
+        L.pqo_decode_column_store.argtypes = [C.POINTER(abi.ChunkJob), C.c_int, C.c_int, C.POINTER(StoreRG)]
+        L.pqo_free_store.argtypes = [C.POINTER(StoreRG), C.c_int]
+        L.pqo_pack_levels.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_void_p]
+        L.pqo_go_roundupsize.argtypes = [C.c_int64]
+        L.pqo_go_roundupsize.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -154,3 +165,35 @@ def assemble_list(def_levels, rep_levels, values, max_def, list_def, elem_def, v
     rows, el = a.num_rows, a.num_elements
     return (lv[:(rows + 7) // 8], lo[:rows + 1], ev[:(el + 7) // 8], evals[:el * value_width],
             (rows, el, a.num_valid, a.null_lists))
+
+
+def decode_column_store(jobs, quirks):
+    """The reference's ColumnStore.values contents per row group (Q1/Q2 triage):
+    list of (status, values bytes (entries x width), nil flags u8)."""
+    n = len(jobs)
+    arr = (abi.ChunkJob * max(n, 1))(*jobs)
+    out = (StoreRG * max(n, 1))()
+    rc = lib().pqo_decode_column_store(arr, n, quirks, out)
+    assert rc == 0, rc
+    res = []
+    for i in range(n):
+        o = out[i]
+        if o.status != 0:
+            res.append((o.status, None, None))
+            continue
+        cnt = o.entries
+        vals = np.ctypeslib.as_array(C.cast(o.values, C.POINTER(C.c_uint8)), shape=(max(cnt * o.value_width, 1),))
+        nil = np.ctypeslib.as_array(C.cast(o.nil_flags, C.POINTER(C.c_uint8)), shape=(max(cnt, 1),))
+        res.append((0, vals[:cnt * o.value_width].copy(), nil[:cnt].copy()))
+    lib().pqo_free_store(out, n)
+    return res
+
+
+def pack_levels(levels, max_level):
+    """packedArray bytes of `levels` (packed_array.go:34-101)."""
+    lv = np.ascontiguousarray(levels, dtype=np.uint8)
+    bw = int(max_level).bit_length()
+    out = np.zeros(max((len(lv) + 7) // 8 * bw, 1), np.uint8)
+    rc = lib().pqo_pack_levels(lv.ctypes.data if len(lv) else None, len(lv), max_level, out.ctypes.data)
+    assert rc == 0
+    return out[:(len(lv) + 7) // 8 * bw]

@@ -344,6 +344,35 @@ int list_launch(hipStream_t s, const pqg_list_args* a, int64_t* seg_scratch, int
   return hipGetLastError() == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 }
 
+// ---------------------------------------------------------------------------
+// ColumnStore refill: levels -> packedArray bytes (packed_array.go:34-101).
+// One lane per group of 8 levels: one 8-byte load, the 8 w-bit fields OR-ed
+// into a 64-bit word (bw <= 8 for u8 levels), bw byte stores.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_pack_levels(const uint8_t* levels_, int64_t n, int bw, uint8_t* packed_) {
+  const PQG_G uint8_t* levels = gconst(levels_);
+  PQG_G uint8_t* packed = gmut(packed_);
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t groups = (n + 7) / 8;
+  if (g >= groups) return;
+  uint64_t bits = 0;
+  const uint64_t mask = (1ull << bw) - 1;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int64_t i = g * 8 + k;
+    const uint64_t v = i < n ? levels[i] : 0;
+    bits |= (v & mask) << (k * bw);
+  }
+  for (int b = 0; b < bw; b++) packed[g * bw + b] = (uint8_t)(bits >> (8 * b));
+}
+
+int pack_levels_launch(hipStream_t s, const uint8_t* levels, int64_t n, int bw, uint8_t* packed) {
+  const int64_t groups = (n + 7) / 8;
+  if (groups > 0 && bw > 0)
+    hipLaunchKernelGGL(k_pack_levels, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, levels, n, bw, packed);
+  return hipGetLastError() == hipSuccess ? PQG_OK : PQG_ERR_HIP;
+}
+
 // Host launcher (called from pqg_assemble in pqg_runtime.hip).  seg_scratch
 // holds 2 × nseg int64; tot 2 int64 (device).
 int assemble_launch(hipStream_t s, const pqg_assemble_args* a, int64_t* seg_scratch, int64_t* tot) {

@@ -21,6 +21,7 @@
 namespace pqg {
 int assemble_launch(hipStream_t s, const pqg_assemble_args* a, int64_t* seg_scratch, int64_t* tot);  // pqg_assemble.hip
 int list_launch(hipStream_t s, const pqg_list_args* a, int64_t* seg_scratch, int64_t* tot);          // pqg_assemble.hip
+int pack_levels_launch(hipStream_t s, const uint8_t* levels, int64_t n, int bw, uint8_t* packed);     // pqg_assemble.hip
 }
 
 namespace pqg {
@@ -142,6 +143,8 @@ struct pqg_ctx {
   DevBuf cand_list, vlists;
   DevBuf asm_seg;  // K8 per-segment counts + totals
   DevBuf offs_arena, doffs_arena;  // K7: value offsets (int64), dictionary record starts
+  DevBuf page_stage;               // pqg_decode_page: [dictionary page][data page]
+  DevBuf blk_src, blk_dst, blk_meta;  // pqg_block_decompress
   int64_t total_tiles = 0;
   JobDev* h_jobs = nullptr;  // pinned
   int h_jobs_cap = 0;
@@ -212,7 +215,8 @@ void pqg_ctx_destroy(pqg_ctx* c) {
   for (auto& e : c->ev) hipEventDestroy(e);
   for (DevBuf* b : {&c->jobs, &c->pages, &c->list, &c->counters, &c->def_arena, &c->rep_arena, &c->value_arena,
                     &c->scratch, &c->streams, &c->runs, &c->blks, &c->cand_list, &c->vlists, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
-                    &c->ok2slot, &c->order, &c->asm_seg, &c->offs_arena, &c->doffs_arena})
+                    &c->ok2slot, &c->order, &c->asm_seg, &c->offs_arena, &c->doffs_arena, &c->page_stage,
+                    &c->blk_src, &c->blk_dst, &c->blk_meta})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
   hipStreamDestroy(c->stream);
@@ -450,6 +454,7 @@ int pqg_decode_chunks_async(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs) {
     if (d.max_def < 0 || d.max_def > 255 || d.max_rep < 0 || d.max_rep > 255) return PQG_ERR_INVALID_ARG;
     if (jobs[i].data_len < 0 || jobs[i].total_compressed_size < 0 || (!jobs[i].data && jobs[i].data_len > 0))
       return PQG_ERR_INVALID_ARG;
+    if (jobs[i].quirks != 0) return PQG_ERR_INVALID_ARG;  // spec-correct only (quirks: oracle triage mode)
   }
   c->cur.assign(jobs, jobs + n_jobs);
   c->n_jobs = n_jobs;
@@ -574,6 +579,112 @@ int pqg_decode_chunks(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs, pqg_chu
   int e = pqg_decode_chunks_async(c, jobs, n_jobs);
   if (e) return e;
   return pqg_sync(c, results, n_jobs);
+}
+
+int pqg_decode_page(pqg_ctx* c, const pqg_page_job* pj, pqg_chunk_result* result) {
+  if (!c || !pj || !result || !pj->page || pj->page_len <= 0 || pj->dict_page_len < 0 ||
+      (pj->dict_page_len > 0 && !pj->dict_page))
+    return PQG_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  const int64_t dl = pj->dict_page ? pj->dict_page_len : 0, total = dl + pj->page_len;
+  // the page (after its dictionary) as a one-page column chunk
+  if (c->page_stage.grow((size_t)total + 64)) return PQG_ERR_HIP;
+  uint8_t* st = (uint8_t*)c->page_stage.p;
+  if ((dl && hipMemcpyAsync(st, pj->dict_page, (size_t)dl, hipMemcpyDeviceToDevice, c->stream) != hipSuccess) ||
+      hipMemcpyAsync(st + dl, pj->page, (size_t)pj->page_len, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+    return PQG_ERR_HIP;
+  pqg_chunk_job job;
+  memset(&job, 0, sizeof(job));
+  job.col = pj->col;
+  job.data = st;
+  job.data_len = total;
+  job.total_compressed_size = total;
+  job.data_page_offset = dl;
+  job.total_uncompressed_size = total;
+  return pqg_decode_chunks(c, &job, 1, result);
+}
+
+int pqg_block_decompress(pqg_ctx* c, int codec, const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap,
+                         int64_t* out_len) {
+  if (!c || (!src && n > 0) || n < 0 || n > INT32_MAX || !out_len) return PQG_ERR_INVALID_ARG;
+  *out_len = 0;
+  if (codec == PQG_CODEC_UNCOMPRESSED) {
+    *out_len = n;
+    if (n > cap) return PQG_ERR_CAPACITY;
+    if (n) memcpy(dst, src, (size_t)n);
+    return PQG_OK;
+  }
+  if (codec != PQG_CODEC_SNAPPY) return PQG_ERR_UNSUPPORTED;
+  // decodedLen (decode.go:32-43): the varint header, on the host to size the output
+  uint64_t v = 0;
+  int hl = 0;
+  for (unsigned sft = 0;; hl++, sft += 7) {
+    if (hl >= n) return PQG_ERR_SNAPPY;
+    const uint8_t b = src[hl];
+    if (b < 0x80) {
+      if (hl > 9 || (hl == 9 && b > 1)) return PQG_ERR_SNAPPY;
+      v |= sft < 64 ? (uint64_t)b << sft : 0;
+      hl++;
+      break;
+    }
+    if (sft < 64) v |= (uint64_t)(b & 0x7f) << sft;
+  }
+  if (v > 0xffffffffull || v > (uint64_t)INT32_MAX) return PQG_ERR_SNAPPY;
+  *out_len = (int64_t)v;
+  if ((int64_t)v > cap) return PQG_ERR_CAPACITY;
+  hipSetDevice(c->device);
+  // one block = one page of a one-job batch: k_snappy decodes it into scratch
+  if (c->blk_src.grow((size_t)n + 64) || c->blk_dst.grow((size_t)v + 64) ||
+      c->blk_meta.grow(sizeof(JobDev) + sizeof(PageDev) + 64 * sizeof(int)))
+    return PQG_ERR_HIP;
+  JobDev jd;
+  memset(&jd, 0, sizeof(jd));
+  jd.data = (const uint8_t*)c->blk_src.p;
+  jd.data_len = n;
+  jd.tcs = n;
+  jd.codec = PQG_CODEC_SNAPPY;
+  jd.scratch_cap = (int64_t)v + 16;
+  PageDev pd;
+  memset(&pd, 0, sizeof(pd));
+  pd.page_type = PQG_PAGE_DICTIONARY;  // a bare block: no values-decoder check after it
+  pd.csize = (int32_t)n;
+  pd.usize = (int32_t)v;
+  pd.payload_offset = 0;
+  pd.scratch_offset = 0;
+  pd.read_status = kOK;
+  uint8_t* meta = (uint8_t*)c->blk_meta.p;
+  JobDev* djob = (JobDev*)meta;
+  PageDev* dpage = (PageDev*)(meta + sizeof(JobDev));
+  int* ints = (int*)(meta + sizeof(JobDev) + sizeof(PageDev));  // [0] list, [1] total, [2..3] queues
+  int hi[4] = {0, 1, 0, 0};
+  if (hipMemcpyAsync(c->blk_src.p, src, (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(djob, &jd, sizeof(jd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(dpage, &pd, sizeof(pd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(ints, hi, sizeof(hi), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    return PQG_ERR_HIP;
+  hipLaunchKernelGGL((k_snappy<32768, 0>), dim3(1), dim3(64), 0, c->stream, djob, dpage, ints, ints + 1, ints + 2,
+                     (uint8_t*)c->blk_dst.p);
+  hipLaunchKernelGGL((k_snappy<65536, 1>), dim3(1), dim3(64), 0, c->stream, djob, dpage, ints, ints + 1, ints + 3,
+                     (uint8_t*)c->blk_dst.p);
+  if (hipGetLastError() != hipSuccess) return PQG_ERR_HIP;
+  if (hipMemcpyAsync(&pd, dpage, sizeof(pd), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return PQG_ERR_HIP;
+  if (pd.read_status != kOK) return pd.read_status;
+  if (v && (hipMemcpyAsync(dst, c->blk_dst.p, (size_t)v, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess))
+    return PQG_ERR_HIP;
+  return PQG_OK;
+}
+
+int pqg_pack_levels(pqg_ctx* c, const uint8_t* levels, int64_t n, int max_level, uint8_t* packed) {
+  if (!c || n < 0 || max_level < 0 || max_level > 255 || (n > 0 && (!levels || !packed))) return PQG_ERR_INVALID_ARG;
+  hipSetDevice(c->device);
+  int bw = 0;
+  while ((max_level >> bw) != 0) bw++;  // bits.Len16(maxLevel)
+  int e = pqg::pack_levels_launch(c->stream, levels, n, bw, packed);
+  if (e) return e;
+  return hip_ok(hipStreamSynchronize(c->stream));
 }
 
 int pqg_get_pages(pqg_ctx* c, int job, pqg_page_info* out, int cap) {

@@ -40,6 +40,7 @@ STATUS = {
 }
 OK = 0
 ERR_CAPACITY = -20
+STATUS_CODES = {v: k for k, v in STATUS.items()}
 
 FIXED_WIDTH = {BOOLEAN: 1, INT32: 4, INT64: 8, INT96: 12, FLOAT: 4, DOUBLE: 8}
 
@@ -65,8 +66,17 @@ class ChunkJob(C.Structure):
         ("num_values_hint", C.c_int64),
         ("total_uncompressed_size", C.c_int64),
         ("has_dict_page_offset", C.c_int32),
-        ("reserved", C.c_int32),
+        ("quirks", C.c_int32),
     ]
+
+
+QUIRK_Q1_PAGE_NILS, QUIRK_Q2_DICT_ALIAS = 1, 2
+
+
+class PageJob(C.Structure):
+    """pqg_page_job (include/pqgpu.h)."""
+    _fields_ = [("col", ColumnDesc), ("page", C.c_void_p), ("page_len", C.c_int64), ("dict_page", C.c_void_p),
+                ("dict_page_len", C.c_int64)]
 
 
 class ChunkResult(C.Structure):
