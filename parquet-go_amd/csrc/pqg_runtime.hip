@@ -37,7 +37,6 @@ __global__ void k_page_chain(JobDev* jobs, PageDev* pages, const Cand* cands, co
                              const int* idx2slot, const int* ok2slot, int* order);
 __global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs);
 __global__ void k_page_list(JobDev* jobs, int n_jobs, int* list, int list_cap, int* total, int* queues);
-template <int RING, int KIND>
 __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                          uint8_t* scratch);
 __global__ void k_page_setup(JobDev* jobs, PageDev* pages, const int* list, const int* total, uint8_t* scratch,
@@ -368,7 +367,7 @@ static int launch_pipeline(pqg_ctx* c) {
   // page-queue kernels: one wave per page; enough waves per SIMD to hide the
   // dependent HBM reads of the run walks (bounded by VGPRs / LDS per kernel)
   const int waves = c->num_cus * 20;
-  const int snappy_waves = c->num_cus * 4;  // 33 KiB LDS each (65 KiB for the large-block instance)
+  const int snappy_waves = c->num_cus * 2;  // 68 KiB LDS each (64 KiB output history)
   hipStream_t s = c->stream;
   if (c->timed) hipEventRecord(c->ev[0], s);
   const int64_t nt = c->total_tiles;
@@ -400,10 +399,7 @@ static int launch_pipeline(pqg_ctx* c) {
   bool any_comp = false;
   for (int i = 0; i < n; i++) any_comp |= c->cur[(size_t)i].col.codec != PQG_CODEC_UNCOMPRESSED;
   if (any_comp) {
-    hipLaunchKernelGGL((k_snappy<32768, 0>), dim3(snappy_waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 8,
-                       scratch);
-    hipLaunchKernelGGL((k_snappy<65536, 1>), dim3(c->num_cus * 2), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 21,
-                       scratch);
+    hipLaunchKernelGGL(k_snappy, dim3(snappy_waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 8, scratch);
   }
   if (c->timed) hipEventRecord(c->ev[3], s);
   HStream* streams = (HStream*)c->streams.p;
@@ -662,9 +658,7 @@ int pqg_block_decompress(pqg_ctx* c, int codec, const uint8_t* src, int64_t n, u
       hipMemcpyAsync(dpage, &pd, sizeof(pd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(ints, hi, sizeof(hi), hipMemcpyHostToDevice, c->stream) != hipSuccess)
     return PQG_ERR_HIP;
-  hipLaunchKernelGGL((k_snappy<32768, 0>), dim3(1), dim3(64), 0, c->stream, djob, dpage, ints, ints + 1, ints + 2,
-                     (uint8_t*)c->blk_dst.p);
-  hipLaunchKernelGGL((k_snappy<65536, 1>), dim3(1), dim3(64), 0, c->stream, djob, dpage, ints, ints + 1, ints + 3,
+  hipLaunchKernelGGL(k_snappy, dim3(1), dim3(64), 0, c->stream, djob, dpage, ints, ints + 1, ints + 2,
                      (uint8_t*)c->blk_dst.p);
   if (hipGetLastError() != hipSuccess) return PQG_ERR_HIP;
   if (hipMemcpyAsync(&pd, dpage, sizeof(pd), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||

@@ -19,243 +19,596 @@ int prof_read_snappy(unsigned long long* out) {
 #endif
 
 // ============================================================================
-// K2: one wave per compressed block.
+// K2: one wave per compressed block, tags resolved a window at a time.
 //
-// The tag stream is serial (each tag's length decides where the next one
-// starts), so the wave decodes it tag by tag, wave-uniformly; the bytes of a
-// literal or a copy are moved by all lanes at once.  The output is produced in
-// an LDS ring that holds the last RING bytes: every back-reference with
-// offset <= RING reads the ring (snappy's copy-1/copy-2 offsets are < 64 KiB),
-// so no tag waits on HBM.  The ring is flushed to the page's scratch block in
-// 4 KiB pieces with 16-byte stores.  The compressed bytes are read through a
-// 1 KiB LDS window (8 bytes per tag read, one broadcast LDS load).  Copies
-// reaching further back than the ring (copy-4 offsets >= RING) read the
-// already flushed output from L2 after the flush stores have completed.
-//
-// Two instances: RING = 32 KiB for blocks of at most 32 KiB (every offset is
-// inside the ring; 4 waves per CU), RING = 64 KiB for larger blocks.
+// 1. Parse.  Every tag's length is a function of the bytes at its own
+//    position, so each lane parses a tag speculatively at two of the next
+//    kPos = 128 byte positions (lane, 64 + lane), from a 4 KiB LDS window.
+// 2. Chain.  The true tags are the chain 0 -> next(0) -> ...; a scalar loop
+//    follows it with v_readlane (an SGPR lane index), a few cycles per tag,
+//    and marks it in two 64-bit masks.  Tags stay in their parse lanes.
+// 3. Offsets and checks.  A DPP prefix sum over the chain's output lengths
+//    gives every tag its output offset; the reference's checks
+//    (decode_other.go:52, 85) and the batch cut (<= kSpan output bytes,
+//    literal bytes inside the window) are then lane-parallel.
+// 4a. Dense windows (>= kDense tags): the batch's output is 64 lanes x one
+//    16-byte output granule, resolved byte by byte: a literal byte's source
+//    is a window byte; a copy byte's source is the output byte `offset`
+//    before it.  Copies reading bytes of the same batch (the overlapping
+//    run-length form included) are resolved by pointer doubling over a
+//    per-byte source table in LDS (<= 10 rounds, usually 0-2); then every
+//    byte reads its source once, from the window or the history ring.
+// 4b. Sparse windows (long literals, few tags): the tags are moved one at a
+//    time with the fields already parsed — a literal as 16-byte granules,
+//    one per lane, a copy one byte per lane — and the following tags are
+//    taken one at a time too (the next header read ahead of the current
+//    tag's bytes) until a streak of short tags sends the wave back to 1-3.
+// The output history is a 64 KiB LDS ring: every copy-1/copy-2 offset
+// (< 64 KiB) reads it; older bytes (copy-4) come from the flushed output
+// through L2.  The ring leaves for HBM in 16-byte granules with each window
+// refill (whose load wait then also covers the stores) or every 16 KiB.  A
+// literal longer than the window goes from HBM in 4 KiB pieces.
 // ============================================================================
-constexpr int kFlush = 4096;
-constexpr int kSmallRing = 32768;  // blocks up to this size go to the 32 KiB-ring instance
+constexpr int kPos = 128;         // tag positions parsed per window (2 per lane)
+constexpr int kDense = 4;         // tags in a window for the batched byte resolution
+constexpr int kSnWin = 4096;      // compressed-stream window (LDS)
+constexpr int kSnWinNeed = 2048;  // window bytes wanted ahead of the first tag
+constexpr int kSpan = 1024;       // output bytes a batch covers: 64 lanes x one 16-byte granule
+constexpr int kRing = 65536;      // output history kept in LDS
+constexpr int kSnFlush = 16384;   // flush granularity (a wave's stores are waited for at the next loop head)
+constexpr int kLongPiece = 4096;  // literal piece read from HBM
+constexpr int kWinLit = 1024;     // literals up to this many bytes (after the granule prefix) move from the window
 
-template <int RING>
 struct SnapShared {
-  uint8_t ring[RING];
-  uint8_t win[kWin];
+  uint8_t ring[kRing];
+  uint8_t in[kSnWin + 32];
+  int32_t src[kSpan];     // per output byte: [pre, kSpan) same batch, >= kSpan window byte + kSpan, else history
+  uint8_t tmap[kSpan];    // 1 + tag position, at the tag's first output byte
+  u32x2_t tent[kPos];     // per tag position: {output start (relative to the batch's first granule),
+                          //  literal: 0x80000000 | window offset of its bytes; copy: offset}
 };
 
-__device__ __forceinline__ uint32_t l2_load_u32(const PQG_G uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// ---- 64-lane DPP scans (row_shr 1/2/4/8, row_bcast 15/31)
+__device__ __forceinline__ uint32_t dpp_incl_add(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t dpp_incl_max(uint32_t x) {
+  x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true));
+  x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true));
+  x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true));
+  x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true));
+  x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+  x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+  return x;
+}
+// value of the previous lane (0 in lane 0): DPP wave_shr:1
+__device__ __forceinline__ uint32_t dpp_prev(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+  return (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+         ((int64_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32);
 }
 
-// The compressed stream through the LDS window (refilled 16-byte aligned so
-// each lane moves one dwordx4).
-struct SnapIn {
-  gcu8 p;
-  int64_t n;
-  int64_t base;
-  PQG_L uint8_t* lds;
-  __device__ void fill(int64_t at) {
-    const uintptr_t abs = (uintptr_t)(p + at);
-    base = at - (int64_t)(abs & 15);
-    const int l = lane_id();
-    const int64_t off = base + l * 16;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (off >= 0 && off + 16 <= n) {
-      v = ldg16((uintptr_t)(p + off));
-    } else {
-      uint32_t w[4] = {0, 0, 0, 0};
-      for (int k = 0; k < 16; k++) {
-        const int64_t j = off + k;
-        if (j >= 0 && j < n) w[k >> 2] |= (uint32_t)p[j] << (8 * (k & 3));
-      }
-      v = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    __builtin_amdgcn_wave_barrier();
-    sts16(lds + l * 16, v);
-    __builtin_amdgcn_wave_barrier();
-  }
-  // 8 bytes at s (bytes past n read as 0): one broadcast LDS load
-  __device__ __forceinline__ uint64_t peek8(int64_t s) {
-    if (s < base || s + 8 > base + kWin) fill(s);
-    const uint32_t o = (uint32_t)(s - base);
-    const PQG_L uint32_t* q = (const PQG_L uint32_t*)(lds + (o & ~3u));
-    const uint32_t a = q[0], b = q[1], c = q[2];
-    const uint32_t sh = (o & 3) * 8;
-    const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sh), hi = __builtin_amdgcn_alignbit(c, b, sh);
-    return (uint64_t)__builtin_amdgcn_readfirstlane(lo) | (uint64_t)__builtin_amdgcn_readfirstlane(hi) << 32;
-  }
+// One speculative tag at stream position pos (bytes from the LDS window).
+struct Tag {
+  int64_t len;   // output bytes
+  int64_t next;  // position of the following tag (relative to the window's first position)
+  uint32_t info; // copy offset
+  int hdr;
+  bool lit, err;
 };
 
-template <int RING>
-struct SnapOut {
-  PQG_L uint8_t* ring;
+__device__ __forceinline__ Tag parse_tag(const PQG_L uint8_t* in, uint32_t wo, int64_t pos, int64_t slen, int rel) {
+  const PQG_L uint32_t* q = (const PQG_L uint32_t*)(in + (wo & ~3u));
+  const uint32_t a = q[0], b = q[1], c = q[2];
+  const uint32_t sft = (wo & 3) * 8;
+  const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sft), hi = __builtin_amdgcn_alignbit(c, b, sft);
+  const uint32_t tag = lo & 0xff;
+  const uint32_t w4 = (lo >> 8) | (hi << 24);  // bytes 1..4
+  Tag t;
+  t.lit = (tag & 3) == 0;
+  t.info = 0;
+  if (t.lit) {
+    const uint32_t x = tag >> 2;
+    if (x < 60) {
+      t.hdr = 1;
+      t.len = (int64_t)x + 1;
+    } else {
+      const int nb = (int)x - 59;
+      t.hdr = 1 + nb;
+      t.len = (int64_t)(nb == 4 ? w4 : (w4 & ((1u << (8 * nb)) - 1))) + 1;
+    }
+  } else if ((tag & 3) == 1) {
+    t.hdr = 2;
+    t.len = 4 + ((tag >> 2) & 7);
+    t.info = (tag & 0xe0) << 3 | (w4 & 0xff);
+  } else if ((tag & 3) == 2) {
+    t.hdr = 3;
+    t.len = 1 + (tag >> 2);
+    t.info = w4 & 0xffff;
+  } else {
+    t.hdr = 5;
+    t.len = 1 + (tag >> 2);
+    t.info = w4;
+  }
+  t.err = pos + t.hdr > slen;                            // s += n; if s > len(src)
+  if (t.lit) t.err |= t.len > slen - (pos + t.hdr);      // length > len(src)-s
+  t.next = rel + t.hdr + (t.lit ? t.len : 0);
+  return t;
+}
+
+struct SnapBlock {
+  gcu8 src;
+  int64_t slen;
   gu8 dst;
   int64_t dlen;
+  SnapShared* sh;
   int64_t d = 0;        // output bytes produced
-  int64_t flushed = 0;  // output bytes stored to dst
-  static constexpr uint32_t M = RING - 1;
+  int64_t flushed = 0;  // output bytes stored (16-aligned until the end)
+  int64_t in_base = kFarAway;
 
-  // store [flushed, upto) from the ring: 16-byte granules of dst (16-aligned);
-  // a ragged tail is stored bytewise and stored again by the next flush, so
-  // `flushed` stays 16-byte aligned
+  // window [in_base, in_base + kSnWin) over the compressed block, 16-aligned in memory
+  __device__ void fill(int64_t at) {
+    const int lane = lane_id();
+    in_base = at - (int64_t)(((uintptr_t)(src + at)) & 15);
+    uint4 v[kSnWin / 1024];
+#pragma unroll
+    for (int h = 0; h < kSnWin / 1024; h++) {
+      const int64_t g = in_base + 1024 * h + 16 * lane;
+      // a granule holding a byte of [0, slen) is mapped
+      v[h] = (g < slen && g + 16 > 0) ? ldg16((uintptr_t)(src + g)) : make_uint4(0, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int h = 0; h < kSnWin / 1024; h++) sts16(lds_ptr(sh->in) + 1024 * h + 16 * lane, v[h]);
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // store ring granules [flushed, upto) to dst (upto 16-aligned, or the end)
   __device__ void flush(int64_t upto) {
     const int lane = lane_id();
     __builtin_amdgcn_wave_barrier();
     for (int64_t g = flushed + 16 * lane; g < upto; g += 16 * 64) {
-      if (g + 16 <= upto) {
-        const u32x4_t v = *(const PQG_L u32x4_t*)(ring + (g & M));
-        stg16((uintptr_t)(dst + g), make_uint4(v.x, v.y, v.z, v.w));
-      } else {
-        for (int64_t k = g; k < upto; k++) dst[k] = ring[k & M];
-      }
+      const u32x4_t v = *(const PQG_L u32x4_t*)(lds_ptr(sh->ring) + (g & (kRing - 1)));
+      stg16((uintptr_t)(dst + g), make_uint4(v.x, v.y, v.z, v.w));
     }
-    flushed = upto & ~(int64_t)15;
+    flushed = upto;
   }
   __device__ __forceinline__ void maybe_flush() {
-    if (d - flushed >= kFlush) flush(flushed + kFlush * ((d - flushed) / kFlush));
+    const int64_t a = d & ~(int64_t)15;
+    if (a - flushed >= kSnFlush) flush(a);
   }
-};
 
-// Literal of `len` bytes at compressed offset s (len <= dlen - d, s + len <= slen).
-template <int RING>
-__device__ __forceinline__ void snap_literal(SnapIn& in, SnapOut<RING>& out, int64_t s, int64_t len) {
-  const int lane = lane_id();
-  constexpr uint32_t M = RING - 1;
-  int64_t done = 0;
-  while (done < len) {
-    out.maybe_flush();
-    // a piece inside the current window, at most 1 KiB
-    const int64_t at = s + done;
-    if (at < in.base || at >= in.base + kWin) in.fill(at);
-    int64_t piece = in.base + kWin - at;
-    if (piece > len - done) piece = len - done;
-    if (piece > 1024) piece = 1024;
-    const uint32_t wo = (uint32_t)(at - in.base);
-    const int64_t d0 = out.d;
-    for (int64_t j = lane; j < piece; j += 64) out.ring[(uint32_t)(d0 + j) & M] = in.lds[wo + j];
-    out.d += piece;
-    done += piece;
-  }
-}
-
-// Copy of `len` bytes from `off` back (validated: 0 < off <= d, len <= dlen - d).
-template <int RING>
-__device__ __forceinline__ void snap_copy(SnapOut<RING>& out, int64_t off, int64_t len) {
-  const int lane = lane_id();
-  constexpr uint32_t M = RING - 1;
-  out.maybe_flush();
-  const int64_t d0 = out.d;
-  if (off <= RING) {
-    // forward copy with overlap == periodic copy of the `off` bytes before d;
-    // the ring still holds positions [d - RING, d)
-    for (int64_t j = lane; j < len; j += 64) {
-      const int64_t from = d0 - off + (off >= len ? j : j % off);
-      out.ring[(uint32_t)(d0 + j) & M] = out.ring[(uint32_t)from & M];
+  // A literal too long for one batch (or whose bytes leave the window):
+  // pieces of up to kLongPiece bytes straight from the compressed block.
+  __device__ void long_literal(int64_t at, int64_t len) {
+    const int lane = lane_id();
+    constexpr int NG = kLongPiece / 1024;  // granules per lane
+    while (len > 0) {
+      const int64_t a0 = d & ~(int64_t)15;
+      const int pre = (int)(d - a0);
+      const int64_t piece = len < kLongPiece - pre ? len : kLongPiece - pre;
+      const int64_t lim = pre + piece;  // piece bytes are [pre, lim) of the granules from a0
+      uint4 x[NG], y[NG];
+      uint32_t r[NG];
+#pragma unroll
+      for (int j = 0; j < NG; j++) {
+        const int64_t i0 = 1024 * j + 16 * lane;  // granule's first byte (relative to a0)
+        const int64_t s0 = at + i0 - pre;         // block offset of that byte
+        const uintptr_t sa = (uintptr_t)(src + s0);
+        r[j] = (uint32_t)(sa & 15);
+        const int64_t gb0 = s0 - (int64_t)r[j];   // aligned granule holding s0
+        // load an aligned granule only if it holds a byte of the piece
+        const int64_t lo = at + (i0 > pre ? i0 - pre : 0), hi = at + (i0 + 16 < lim ? i0 + 16 : lim) - pre;
+        const bool need = i0 < lim && i0 + 16 > pre;
+        x[j] = (need && gb0 + 16 > lo) ? ldg16(sa & ~(uintptr_t)15) : make_uint4(0, 0, 0, 0);
+        y[j] = (need && r[j] != 0 && gb0 + 16 < hi) ? ldg16((sa & ~(uintptr_t)15) + 16) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < NG; j++) {
+        const int64_t i0 = 1024 * j + 16 * lane;
+        if (i0 >= lim) continue;
+        const uint32_t q[8] = {x[j].x, x[j].y, x[j].z, x[j].w, y[j].x, y[j].y, y[j].z, y[j].w};
+        const uint32_t qd = r[j] >> 2, sft = (r[j] & 3) * 8;
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          uint32_t lo_w = q[k], hi_w = q[k + 1];
+#pragma unroll
+          for (int m = 1; m < 4; m++) {
+            lo_w = qd == (uint32_t)m ? q[m + k] : lo_w;
+            hi_w = qd == (uint32_t)m ? q[m + k + 1 < 8 ? m + k + 1 : 7] : hi_w;
+          }
+          w[k] = __builtin_amdgcn_alignbit(hi_w, lo_w, sft);
+        }
+        const uint32_t rp = (uint32_t)((a0 + i0) & (kRing - 1));
+        if (i0 < pre) {  // the granule's bytes before d are history: keep them
+          const u32x4_t old = *(const PQG_L u32x4_t*)(lds_ptr(sh->ring) + rp);
+          const uint32_t ow[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int e = 0; e < 4; e++) m |= (4 * k + e < pre ? 0xffu : 0u) << (8 * e);
+            w[k] = (ow[k] & m) | (w[k] & ~m);
+          }
+        }
+        sts16(lds_ptr(sh->ring) + rp, make_uint4(w[0], w[1], w[2], w[3]));
+      }
+      __builtin_amdgcn_wave_barrier();
+      d += piece;
+      at += piece;
+      len -= piece;
+      maybe_flush();
     }
-  } else {
-    // older than the ring (copy-4 offsets): the flushed output, read from L2
-    // once the flush stores have completed (off > RING >= 64 > len: no overlap)
-    out.flush(d0);
-    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
-    __builtin_amdgcn_wave_barrier();
-    for (int64_t j = lane; j < len; j += 64) {
-      const uintptr_t a = (uintptr_t)(out.dst + (d0 - off + j));
-      out.ring[(uint32_t)(d0 + j) & M] =
-          (uint8_t)(l2_load_u32((const PQG_G uint32_t*)(a & ~(uintptr_t)3)) >> ((a & 3) * 8));
-    }
   }
-  out.d += len;
-}
 
-// decode_other.go:14-101 over [s, slen) into dlen bytes
-template <int RING>
-__device__ int snappy_body(SnapIn& in, int64_t s, int64_t slen, SnapOut<RING>& out) {
-  const int64_t dlen = out.dlen;
-#ifdef PQG_PROFILE
-  uint64_t n_lit = 0, n_copy = 0, c_lit = 0, c_copy = 0, c_parse = 0;
-#endif
-  while (s < slen) {
-    PQG_T(ta);
-    const uint64_t x8 = in.peek8(s);
-#ifdef PQG_PROFILE
-    PQG_T(tb);
-    c_parse += tb - ta;
-#endif
-    const uint32_t tag = (uint32_t)x8 & 0xff;
-    int64_t length, offset;
-    switch (tag & 3) {
-      case 0: {
+  // A literal of len bytes at window offset wo (len <= kWinLit, inside the window).
+  __device__ __forceinline__ void window_literal(uint32_t wo, int64_t len) {
+    const int lane = lane_id();
+    const int64_t a0 = d & ~(int64_t)15;
+    const int pre = (int)(d - a0);
+    const int lim = pre + (int)len;
+    if (16 * lane < lim) {
+      // source bytes of the granule: window offsets [wo - pre + 16 lane, +16)
+      // (lane 0 may start up to 15 bytes before the window: those bytes are
+      // the granule's history prefix, replaced below; the reads stay in LDS)
+      const int so = (int)wo - pre + 16 * lane;
+      const PQG_L uint32_t* q = (const PQG_L uint32_t*)(lds_ptr(sh->in) + (so & ~3));
+      const uint32_t sft = (uint32_t)(so & 3) * 8;
+      const uint32_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3], x4 = q[4];
+      uint32_t w[4] = {__builtin_amdgcn_alignbit(x1, x0, sft), __builtin_amdgcn_alignbit(x2, x1, sft),
+                       __builtin_amdgcn_alignbit(x3, x2, sft), __builtin_amdgcn_alignbit(x4, x3, sft)};
+      const uint32_t rp = (uint32_t)((a0 + 16 * lane) & (kRing - 1));
+      if (lane == 0 && pre > 0) {  // keep the history bytes before d
+        const u32x4_t old = *(const PQG_L u32x4_t*)(lds_ptr(sh->ring) + rp);
+        const uint32_t ow[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int keep = pre - 4 * k;  // bytes of this dword before d
+          const uint32_t m = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : (0xffffffffu >> (8 * (4 - keep)));
+          w[k] = (ow[k] & m) | (w[k] & ~m);
+        }
+      }
+      sts16(lds_ptr(sh->ring) + rp, make_uint4(w[0], w[1], w[2], w[3]));
+    }
+    d += len;
+  }
+
+  // Copy of len (<= 64) bytes from offset back, one byte per lane.
+  __device__ __forceinline__ void copy_bytes(uint32_t off, int len) {
+    const int lane = lane_id();
+    const int64_t ring_lo = ((d + 15) & ~(int64_t)15) - kRing;  // see below
+    int j = lane;
+    if (off < (uint32_t)len) j = lane % (int)off;  // overlapping: the period of `off` bytes before d
+    const int64_t h = d - (int64_t)off + j;
+    if ((int64_t)(d - off) >= ring_lo) {
+      const uint8_t b = lds_ptr(sh->ring)[(uint32_t)h & (kRing - 1)];
+      if (lane < len) lds_ptr(sh->ring)[(uint32_t)(d + lane) & (kRing - 1)] = b;
+    } else {
+      // older than the ring (copy-4): the flushed output through L2, once the
+      // flush stores have landed and this CU's L1 holds no stale line
+      // (off > kRing - 16 > len: no overlap)
+      flush(d & ~(int64_t)15);
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      uint8_t b = 0;
+      if (lane < len) b = dst[h];
+      if (lane < len) lds_ptr(sh->ring)[(uint32_t)(d + lane) & (kRing - 1)] = b;
+    }
+    d += len;
+  }
+
+  // 8 bytes at block offset t (inside the window): one broadcast LDS load
+  __device__ __forceinline__ uint64_t peek8(int64_t t) {
+    const uint32_t o = (uint32_t)(t - in_base);
+    const PQG_L uint32_t* q = (const PQG_L uint32_t*)(lds_ptr(sh->in) + (o & ~3u));
+    const uint32_t a = q[0], b = q[1], c = q[2];
+    const uint32_t sft = (o & 3) * 8;
+    const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sft), hi = __builtin_amdgcn_alignbit(c, b, sft);
+    return (uint64_t)__builtin_amdgcn_readfirstlane(lo) | (uint64_t)__builtin_amdgcn_readfirstlane(hi) << 32;
+  }
+
+  // Up to max tags one at a time (tag-sparse stretches: long literals), the
+  // next tag's header read ahead of the current tag's bytes.  Returns to the
+  // windowed resolution after a streak of short tags or at a window refill.
+  // kOK, or kSNAPPY at a corrupt tag.
+  __device__ int serial(int64_t& s, int max) {
+    int short_streak = 0;
+    uint64_t x8 = peek8(s);
+    for (int n = 0; n < max && s < slen && short_streak < 4; n++) {
+      const uint32_t tag = (uint32_t)x8 & 0xff;
+      int64_t length, ns;
+      uint32_t offset = 0;
+      const bool lit = (tag & 3) == 0;
+      int hdr;
+      if (lit) {
         uint32_t x = tag >> 2;
-        if (x < 60) {
-          s += 1;
-        } else {
+        hdr = 1;
+        if (x >= 60) {
           const int nb = (int)x - 59;  // 1..4 length bytes
-          s += 1 + nb;
-          if ((uint64_t)s > (uint64_t)slen) return kSNAPPY;
+          hdr = 1 + nb;
+          if (s + hdr > slen) return kSNAPPY;
           x = (uint32_t)(x8 >> 8) & (nb == 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1));
         }
         length = (int64_t)x + 1;
-        if (length > dlen - out.d || length > slen - s) return kSNAPPY;
-        snap_literal(in, out, s, length);
-#ifdef PQG_PROFILE
-        {
-          PQG_T(tc);
-          c_lit += tc - tb;
-          n_lit++;
+        if (length > dlen - d || length > slen - (s + hdr)) return kSNAPPY;
+        ns = s + hdr + length;
+      } else {
+        hdr = (tag & 3) == 1 ? 2 : (tag & 3) == 2 ? 3 : 5;
+        if (s + hdr > slen) return kSNAPPY;
+        if ((tag & 3) == 1) {
+          length = 4 + ((tag >> 2) & 7);
+          offset = (tag & 0xe0) << 3 | ((uint32_t)(x8 >> 8) & 0xff);
+        } else if ((tag & 3) == 2) {
+          length = 1 + (tag >> 2);
+          offset = (uint32_t)(x8 >> 8) & 0xffff;
+        } else {
+          length = 1 + (tag >> 2);
+          offset = (uint32_t)(x8 >> 8);
         }
-#endif
-        s += length;
+        if (offset == 0 || (int64_t)offset > d || length > dlen - d) return kSNAPPY;
+        ns = s + hdr;
+      }
+      short_streak = length < 16 ? short_streak + 1 : 0;
+      const bool next_in = ns < slen && ns >= in_base && ns + kSnWinNeed <= in_base + kSnWin;
+      const uint64_t nx8 = next_in ? peek8(ns) : 0;
+      if (lit) {
+        const int64_t at = s + hdr;
+        if ((d & 15) + length <= kWinLit && at + length <= in_base + kSnWin) window_literal((uint32_t)(at - in_base), length);
+        else long_literal(at, length);
+      } else {
+        copy_bytes(offset, (int)length);
+      }
+      s = ns;
+      if (!next_in) break;
+      x8 = nx8;
+    }
+    if ((d & ~(int64_t)15) - flushed >= kSnFlush) flush(d & ~(int64_t)15);
+    return kOK;
+  }
+
+  // decode_other.go:14-101 from tag position s (after the length varint).
+  // The ring holds output [ring_lo, d), ring_lo = roundup16(d) - kRing: a
+  // ragged last granule overwrites the slots of the kRing-older bytes just
+  // above d.
+  __device__ int run(int64_t s) {
+    const int lane = lane_id();
+    const PQG_L uint8_t* IN = lds_ptr(sh->in);
+    int serial_next = 0;  // tags to take one at a time before the next windowed resolution
+    while (s < slen) {
+      if (s < in_base || s + kSnWinNeed > in_base + kSnWin) {
+        // pending output goes out with the window loads: one wait covers both
+        if ((d & ~(int64_t)15) - flushed >= 2048) flush(d & ~(int64_t)15);
+        fill(s);
+      }
+      if (serial_next > 0) {
+        const int e = serial(s, serial_next);
+        if (e) return e;
+        serial_next = 0;
         continue;
       }
-      case 1:
-        s += 2;
-        if ((uint64_t)s > (uint64_t)slen) return kSNAPPY;
-        length = 4 + ((tag >> 2) & 7);
-        offset = (int64_t)((tag & 0xe0) << 3 | ((uint32_t)(x8 >> 8) & 0xff));
-        break;
-      case 2:
-        s += 3;
-        if ((uint64_t)s > (uint64_t)slen) return kSNAPPY;
-        length = 1 + (tag >> 2);
-        offset = (int64_t)((uint32_t)(x8 >> 8) & 0xffff);
-        break;
-      default:
-        s += 5;
-        if ((uint64_t)s > (uint64_t)slen) return kSNAPPY;
-        length = 1 + (tag >> 2);
-        offset = (int64_t)(uint32_t)(x8 >> 8);
-        break;
+      // ---- 1. speculative tags at positions lane and 64 + lane
+      const uint32_t wo = (uint32_t)(s - in_base) + lane;
+      const Tag t0 = parse_tag(IN, wo, s + lane, slen, lane);
+      const Tag t1 = parse_tag(IN, wo + 64, s + 64 + lane, slen, 64 + lane);
+      const int n0 = (t0.err || t0.next >= kPos) ? kPos : (int)t0.next;
+      const int n1 = (t1.err || t1.next >= kPos) ? kPos : (int)t1.next;
+      // ---- 2. the chain, one v_readlane per tag
+      uint64_t cm0 = 0, cm1 = 0;
+      int p = 0, last = 0;
+      const int64_t lim = slen - s;  // tags start before the end of the block
+      while (p < kPos && p < lim) {
+        last = p;
+        const int l = p & 63;
+        const int r0 = __builtin_amdgcn_readlane(n0, l), r1 = __builtin_amdgcn_readlane(n1, l);
+        if (p < 64) {
+          cm0 |= 1ull << l;
+          p = r0;
+        } else {
+          cm1 |= 1ull << l;
+          p = r1;
+        }
+      }
+      const bool on0 = (cm0 >> lane) & 1, on1 = (cm1 >> lane) & 1;
+      // ---- 3. output offsets and the reference's checks
+      const uint32_t o0 = on0 ? (uint32_t)(t0.len < (1 << 30) ? t0.len : (1 << 30)) : 0u;
+      const uint32_t o1 = on1 ? (uint32_t)(t1.len < (1 << 30) ? t1.len : (1 << 30)) : 0u;
+      const uint32_t i0 = dpp_incl_add(o0);
+      const uint32_t tot0 = (uint32_t)__builtin_amdgcn_readlane((int)i0, 63);
+      const uint32_t i1 = dpp_incl_add(o1) + tot0;
+      const int64_t st0 = (int64_t)(i0 - o0), st1 = (int64_t)(i1 - o1);  // output offsets (relative to d)
+      const int64_t a0 = d & ~(int64_t)15;
+      const int pre = (int)(d - a0);
+      auto check = [&](const Tag& t, int64_t st, int64_t pos, bool& cut) {
+        const int64_t dt = d + st;
+        bool e = t.err || t.len > dlen - dt;                       // length > len(dst)-d
+        if (!t.lit) e |= t.info == 0 || (int64_t)t.info > dt;       // offset <= 0 || d < offset
+        cut = pre + st + t.len > kSpan || (t.lit && pos + t.hdr + t.len > in_base + kSnWin);
+        return e;
+      };
+      bool c0, c1;
+      const bool e0 = check(t0, st0, s + lane, c0), e1 = check(t1, st1, s + 64 + lane, c1);
+      if (__ballot(on0 && e0) | __ballot(on1 && e1)) return kSNAPPY;
+      const uint64_t cb0 = __ballot(on0 && c0), cb1 = __ballot(on1 && c1);
+      const int cutpos = cb0 ? __ffsll((long long)cb0) - 1 : cb1 ? 64 + __ffsll((long long)cb1) - 1 : kPos;
+      if (cutpos == 0) {
+        // tag 0 alone is too long for a batch: a literal (copies are <= 64 bytes)
+        const int64_t l0 = readlane64(t0.len, 0);
+        const int64_t at0 = s + __builtin_amdgcn_readlane(t0.hdr, 0);
+        long_literal(at0, l0);
+        s = at0 + l0;
+        serial_next = 64;
+        continue;
+      }
+      // ---- the chain's tags before cutpos; output [d, d1)
+      const bool b0 = on0 && lane < cutpos, b1 = on1 && 64 + lane < cutpos;
+      const uint64_t bm0 = __ballot(b0), bm1 = __ballot(b1);
+      int64_t out, s1;
+      if (cutpos < kPos) {
+        const int l = cutpos & 63;
+        out = cutpos < 64 ? (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(i0 - o0), l)
+                          : (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(i1 - o1), l);
+        s1 = s + cutpos;
+      } else {
+        out = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)i1, 63);
+        s1 = s + readlane64(last < 64 ? t0.next : t1.next, last & 63);
+      }
+      const int64_t d1 = d + out;
+      if (__popcll(bm0) + __popcll(bm1) < kDense) {
+        // ---- 4b. sparse: tag by tag, with the fields already parsed
+        uint64_t m0 = bm0, m1 = bm1;
+        while (m0 | m1) {
+          const bool hi = m0 == 0;
+          const int l = __ffsll((long long)(hi ? m1 : m0)) - 1;
+          if (hi) m1 &= m1 - 1;
+          else m0 &= m0 - 1;
+          const int64_t len = readlane64(hi ? t1.len : t0.len, l);
+          const bool lit = __builtin_amdgcn_readlane((int)(hi ? t1.lit : t0.lit), l) != 0;
+          if (lit) {
+            const int64_t at = s + (hi ? 64 : 0) + l + __builtin_amdgcn_readlane(hi ? t1.hdr : t0.hdr, l);
+            if ((d & 15) + len <= kWinLit) window_literal((uint32_t)(at - in_base), len);
+            else long_literal(at, len);
+          } else {
+            copy_bytes((uint32_t)__builtin_amdgcn_readlane((int)(hi ? t1.info : t0.info), l), (int)len);
+          }
+        }
+        s = s1;
+        if ((d & ~(int64_t)15) - flushed >= kSnFlush) flush(d & ~(int64_t)15);
+        serial_next = 64;  // a tag-sparse stretch: continue tag by tag
+        continue;
+      }
+      // ---- 4a. dense: per-byte sources for the granules from a0
+      const int end = pre + (int)out;  // batch bytes [pre, end)
+      PQG_L uint8_t* TM = lds_ptr(sh->tmap);
+      *(PQG_L u32x4_t*)(TM + 16 * lane) = u32x4_t{0u, 0u, 0u, 0u};
+      __builtin_amdgcn_wave_barrier();
+      PQG_L u32x2_t* TE = lds_ptr(sh->tent);
+      if (b0) {
+        TE[lane] = u32x2_t{(uint32_t)(pre + (int)st0),
+                           t0.lit ? (0x80000000u | (uint32_t)(s + lane + t0.hdr - in_base)) : t0.info};
+        TM[pre + st0] = (uint8_t)(lane + 1);
+      }
+      if (b1) {
+        TE[64 + lane] = u32x2_t{(uint32_t)(pre + (int)st1),
+                                t1.lit ? (0x80000000u | (uint32_t)(s + 64 + lane + t1.hdr - in_base)) : t1.info};
+        TM[pre + st1] = (uint8_t)(65 + lane);
+      }
+      __builtin_amdgcn_wave_barrier();
+      // tag of each of this lane's 16 bytes: running max of the marks, then
+      // the exclusive max over the lanes before
+      const u32x4_t mk = *(const PQG_L u32x4_t*)(TM + 16 * lane);
+      const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
+      uint32_t tix[16];
+      uint32_t run_max = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const uint32_t m = (mw[k >> 2] >> (8 * (k & 3))) & 0xff;
+        run_max = m > run_max ? m : run_max;
+        tix[k] = run_max;
+      }
+      const uint32_t before = dpp_prev(dpp_incl_max(run_max));
+      int32_t own[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const int idx = 16 * lane + k;
+        const uint32_t t = (tix[k] > before ? tix[k] : before) - 1;
+        const u32x2_t te = TE[t & (kPos - 1)];  // one load for both fields: no load under a branch
+        const int32_t st = (int32_t)te.x;
+        const uint32_t inf = te.y;
+        const int32_t v = (inf & 0x80000000u) ? kSpan + (int32_t)(inf & 0x7fffffffu) + (idx - st) : idx - (int32_t)inf;
+        // history bytes before d stay as they are; bytes past the batch read any terminal
+        own[k] = idx < pre ? idx : idx >= end ? kSpan : v;
+      }
+      // same-batch copy sources: pointer doubling over src[]
+      bool chase = false;
+#pragma unroll
+      for (int k = 0; k < 16; k++) chase |= own[k] >= pre && own[k] < kSpan;
+      if (__ballot(chase)) {
+        PQG_L int32_t* S = lds_ptr(sh->src);
+        for (int r = 0; r < 11; r++) {
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            *(PQG_L u32x4_t*)(S + 16 * lane + 4 * k) =
+                u32x4_t{(uint32_t)own[4 * k], (uint32_t)own[4 * k + 1], (uint32_t)own[4 * k + 2],
+                        (uint32_t)own[4 * k + 3]};
+          __builtin_amdgcn_wave_barrier();
+          chase = false;
+#pragma unroll
+          for (int k = 0; k < 16; k++) {
+            // unconditional loads (a guarded load would wait on its own)
+            const bool in = own[k] >= pre && own[k] < kSpan;
+            const int32_t nv = S[in ? own[k] : 0];
+            own[k] = in ? nv : own[k];
+            chase |= own[k] >= pre && own[k] < kSpan;
+          }
+          __builtin_amdgcn_wave_barrier();
+          if (!__ballot(chase)) break;
+        }
+      }
+      // every byte reads its source once: the window or the ring (one LDS
+      // byte load at a computed address), or, older than the ring, L2
+      const int64_t ring_lo = ((d + 15) & ~(int64_t)15) - kRing;
+      const PQG_L uint8_t* shb = (const PQG_L uint8_t*)lds_ptr(sh->ring);  // the ring is at offset 0
+      const uint32_t in_off = (uint32_t)(IN - shb);
+      uint32_t bt[16];
+      bool far = false;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        const int32_t v = own[k];
+        const int64_t h = a0 + v;
+        const uint32_t off = v >= kSpan ? in_off + (uint32_t)(v - kSpan) : (uint32_t)(h & (kRing - 1));
+        far |= v < kSpan && h < ring_lo;
+        bt[k] = shb[off];
+      }
+      if (__ballot(far)) {
+        // flushed output, read through L2: wait for the flush stores, then
+        // invalidate this CU's L1 (a line loaded earlier may hold bytes that
+        // were stored after it was cached)
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        uint32_t fw[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+          const int64_t h = a0 + own[k];
+          const bool f = own[k] < kSpan && h < ring_lo;
+          fw[k] = *(const PQG_G uint32_t*)((uintptr_t)(dst + (f ? h : 0)) & ~(uintptr_t)3);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+          const int64_t h = a0 + own[k];
+          if (own[k] < kSpan && h < ring_lo) bt[k] = (fw[k] >> (((uintptr_t)(dst + h) & 3) * 8)) & 0xff;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (16 * lane < end) {
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) w[k] = bt[4 * k] | bt[4 * k + 1] << 8 | bt[4 * k + 2] << 16 | bt[4 * k + 3] << 24;
+        sts16(lds_ptr(sh->ring) + ((a0 + 16 * lane) & (kRing - 1)), make_uint4(w[0], w[1], w[2], w[3]));
+      }
+      __builtin_amdgcn_wave_barrier();
+      d = d1;
+      s = s1;
+      maybe_flush();
     }
-    if (offset <= 0 || out.d < offset || length > dlen - out.d) return kSNAPPY;
-    snap_copy(out, offset, length);
-#ifdef PQG_PROFILE
-    {
-      PQG_T(tc);
-      c_copy += tc - tb;
-      n_copy++;
-    }
-#endif
+    if (d != dlen) return kSNAPPY;
+    flush((dlen + 15) & ~(int64_t)15);
+    return kOK;
   }
-#ifdef PQG_PROFILE
-  PQG_ACC(16, 0, n_lit);
-  PQG_ACC(17, 0, n_copy);
-  PQG_ACC(18, 0, c_lit);
-  PQG_ACC(19, 0, c_copy);
-  PQG_ACC(20, 0, c_parse);
-  PQG_ACC(21, 0, slen);
-  PQG_ACC(22, 0, dlen);
-#endif
-  if (out.d != dlen) return kSNAPPY;
-  out.flush(dlen);
-  return kOK;
-}
+};
 
-// kind 0: blocks of at most kSmallRing bytes; kind 1: larger ones
-template <int RING, int KIND>
 __global__ void __launch_bounds__(64) k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total,
                                                int* queue, uint8_t* scratch) {
-  __shared__ __attribute__((aligned(16))) SnapShared<RING> sh;
+  __shared__ __attribute__((aligned(16))) SnapShared sh;
   const int lane = lane_id();
   for (;;) {
     const int t = queue_next(queue);
@@ -272,18 +625,18 @@ __global__ void __launch_bounds__(64) k_snappy(JobDev* jobs, PageDev* pages, con
       clen = (int32_t)((uint32_t)pg.csize - (uint32_t)levels);
       ulen = (int32_t)((uint32_t)pg.usize - (uint32_t)levels);
     }
-    if ((KIND == 0) != (ulen <= kSmallRing)) continue;  // the other instance's block
     const JobDev job = jobs[pg.job];
-    SnapIn in{gconst(job.data) + src_off, clen, kFarAway, lds_ptr(sh.win)};
+    SnapBlock blk{gconst(job.data) + src_off, clen, gmut(scratch) + job.scratch_base + pg.scratch_offset, ulen, &sh};
     // decodedLen: binary.Uvarint over the block (decode.go:32-43)
     uint64_t v = 0;
     int hl = 0;
     int e = kOK;
     {
+      blk.fill(0);
       unsigned sft = 0;
       for (int i = 0;; i++) {
         if (i >= clen) { e = kSNAPPY; break; }
-        const int b = (int)(in.peek8(i) & 0xff);
+        const int b = lds_ptr(sh.in)[i - blk.in_base];
         if (b < 0x80) {
           if (i > 9 || (i == 9 && b > 1)) e = kSNAPPY;
           else v |= (sft < 64 ? (uint64_t)b << sft : 0);
@@ -296,17 +649,11 @@ __global__ void __launch_bounds__(64) k_snappy(JobDev* jobs, PageDev* pages, con
     }
     if (e == kOK && v > 0xffffffffull) e = kSNAPPY;
     if (e == kOK && (int64_t)v != ulen) e = kSIZE;
-    if (e == kOK) {
-      SnapOut<RING> out{lds_ptr(sh.ring), gmut(scratch) + job.scratch_base + pg.scratch_offset, ulen};
-      e = snappy_body(in, hl, clen, out);
-    }
+    if (e == kOK) e = blk.run(hl);
     // V1: getValuesDecoder runs after the block is decompressed (page_v1.go:91-97)
     if (e == kOK && pg.page_type == 0 && !values_supported(job.type, job.type_length, pg.encoding)) e = kUNSUPPORTED;
     if (lane == 0 && e != kOK) pages[pidx].read_status = e;
   }
 }
-
-template __global__ void k_snappy<32768, 0>(JobDev*, PageDev*, const int*, const int*, int*, uint8_t*);
-template __global__ void k_snappy<65536, 1>(JobDev*, PageDev*, const int*, const int*, int*, uint8_t*);
 
 }  // namespace pqg
