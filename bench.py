@@ -41,7 +41,7 @@ for p in (ROOT, os.path.join(ROOT, "parquet-go_amd")):
 
 METRIC = "decoded GB/s (uncompressed output) per GPU & node at 1/2/4/8; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-STAGES = ["scan", "list", "snappy", "setup", "walk", "levels", "nn_scan", "values", "strings", "finalize"]
+STAGES = ["scan", "list", "snappy", "levels", "walk", "unused", "nn_scan", "values", "strings", "finalize"]
 PROFILE_TAG = "r02"
 
 
@@ -170,7 +170,6 @@ def account(wl, dec, res):
                 if meta.codec != 0:
                     lv2 = lv if pg.page_type == 3 else 0
                     st["snappy"] += pg.compressed_size - lv2 + pg.uncompressed_size - lv2
-            st["walk"] += lev_in
             st["levels"] += lev_in + slots_out
             st["values" if r.value_width else "strings"] += val_in + dict_in + vout
             ji += 1
@@ -257,8 +256,8 @@ def cpu_baseline(wl, seconds):
 
 # ---------------------------------------------------------------- PMC traffic (committed passes)
 STAGE_KERNELS = {"scan": ["k_page_cands", "k_cand_parse", "k_tile_scan", "k_cand_link", "k_page_chain",
-                          "k_scan_pages"], "list": ["k_page_list"], "snappy": ["k_snappy"], "setup": ["k_page_setup"],
-                 "walk": ["k_hybrid_walk"], "levels": ["k_levels_expand"], "nn_scan": ["k_nn_scan"],
+                          "k_scan_pages"], "list": ["k_page_list"], "snappy": ["k_snappy"], "levels": ["k_page_levels"],
+                 "walk": ["k_hybrid_walk"], "unused": [], "nn_scan": ["k_nn_scan"],
                  "values": ["k_values"], "strings": ["k_str_dict", "k_str_plain", "k_str_count", "k_char_scan",
                                                   "k_str_copy"],
                  "finalize": ["k_finalize"]}

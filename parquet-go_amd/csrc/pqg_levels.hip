@@ -1,20 +1,17 @@
-// pqg_levels.hip — K3: page streams, the RLE/bit-packed hybrid run walk and
-// the level expansion.
+// pqg_levels.hip — K3: page setup, level decode, the RLE/bit-packed hybrid
+// run walk of the value streams, and the notNull scan.
 //
-//   K3a k_page_setup     one lane per page: the read phase of the level
-//                        streams (V1 initSize: page_v1.go:99-105,
-//                        hybrid_decoder.go:57-67; V2 raw level bytes:
-//                        page_v2.go:103-121) and registration of every hybrid
-//                        stream of the page (levels, dictionary indices
-//                        type_dict.go:22-37, RLE booleans type_boolean.go:100-120)
-//   K3b k_hybrid_walk    one LANE per hybrid stream: the serial run-header walk
-//                        of hybridDecoder.next (hybrid_decoder.go:82-166) writes
-//                        a run table and a block index.  The walk is the only
-//                        serial part of the format; giving each lane its own
-//                        stream keeps all 64 lanes busy on it.
-//   K3c k_levels_expand  one wave per page: rep then def levels, 8 values per
-//                        lane per 512-value block, notNull = #(def == maxD)
-//                        (decodePackedArray helpers.go:131-147)
+//   K3a k_page_levels    one wave per data page: the read phase of the page
+//                        (V1 initSize: page_v1.go:99-105, hybrid_decoder.go:57-67;
+//                        V2 raw level bytes: page_v2.go:103-121), registration
+//                        of its value stream (dictionary indices
+//                        type_dict.go:22-37, RLE booleans type_boolean.go:100-120),
+//                        then rep and def levels decoded straight into the level
+//                        arenas (hybridDecoder.next, hybrid_decoder.go:82-166;
+//                        decodePackedArray helpers.go:131-147), notNull = #(def == maxD)
+//   K3b k_hybrid_walk    one LANE per value stream: the serial run-header walk
+//                        writes a run table and a block index for the values
+//                        kernels (pqg_hybrid.h)
 //   K3d k_nn_scan        per chunk: value offsets = exclusive scan of notNull
 //                        (readPageData chunk_reader.go:380-402) and the
 //                        dictionary page (page_dict.go:30-64)
@@ -64,100 +61,6 @@ __device__ __forceinline__ int reg_stream(JobDev& job, HStream* streams, int32_t
   S.n_blocks = 0;
   *slot = id;
   return id;
-}
-
-__global__ void __launch_bounds__(256) k_page_setup(JobDev* jobs, PageDev* pages, const int* list, const int* total,
-                                                    uint8_t* scratch, HStream* streams, int* vlists, int* vcount,
-                                                    int list_cap) {
-  const int nt = *total;
-  for (int t = blockIdx.x * 256 + threadIdx.x; t < nt; t += gridDim.x * 256) {
-    const int pidx = list[t];
-    PageDev& pg = pages[pidx];
-    pg.hs_rep = pg.hs_def = pg.hs_val = -1;
-    if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3)) continue;
-    JobDev& job = jobs[pg.job];
-    if (job.status == kCAPACITY) continue;
-    // ---- the page block and its level / value streams (read phase)
-    gcu8 block;
-    int64_t blen;
-    int32_t levels = 0;
-    if (pg.page_type == 3) {
-      levels = (int32_t)((uint32_t)pg.rep_len + (uint32_t)pg.def_len);
-      blen = (int32_t)((uint32_t)pg.csize - (uint32_t)levels);
-      if (pg.scratch_offset >= 0) blen = (int32_t)((uint32_t)pg.usize - (uint32_t)levels);
-    } else {
-      blen = pg.scratch_offset >= 0 ? pg.usize : pg.csize;
-    }
-    if (pg.scratch_offset >= 0) block = gconst(scratch) + job.scratch_base + pg.scratch_offset;
-    else block = gconst(job.data) + pg.payload_offset + (levels > 0 ? levels : 0);
-    gcu8 rep = nullptr, def = nullptr;
-    int64_t rep_n = -1, def_n = -1;  // -1: the level decoder is not initialised
-    int64_t vpos = 0;
-    int e = kOK;
-    if (pg.page_type == 0) {
-      // rDecoder.initSize then dDecoder.initSize (page_v1.go:99-105)
-      if (job.max_rep > 0) {
-        if (blen - vpos < 4) e = kEOF;
-        else {
-          const int64_t sz = rd_u32(block + vpos);
-          const int64_t take = min(sz, blen - vpos - 4);
-          rep = block + vpos + 4;
-          rep_n = take;
-          vpos += 4 + take;
-        }
-      }
-      if (e == kOK && job.max_def > 0) {
-        if (blen - vpos < 4) e = kEOF;
-        else {
-          const int64_t sz = rd_u32(block + vpos);
-          const int64_t take = min(sz, blen - vpos - 4);
-          def = block + vpos + 4;
-          def_n = take;
-          vpos += 4 + take;
-        }
-      }
-    } else {
-      // V2: raw level bytes, a decoder only for a non-empty section (page_v2.go:110-120)
-      gcu8 lv = gconst(job.data) + pg.payload_offset;
-      if (levels > 0 && pg.rep_len > 0) { rep = lv; rep_n = pg.rep_len; }
-      if (levels > 0 && pg.def_len > 0) { def = lv + pg.rep_len; def_n = levels - pg.rep_len; }
-    }
-    if (e != kOK) {
-      pg.read_status = e;
-      continue;
-    }
-    pg.block = (const uint8_t*)block;
-    pg.block_len = blen;
-    pg.val = (const uint8_t*)(block + vpos);
-    pg.val_n = blen - vpos;
-    pg.rep = (const uint8_t*)rep;
-    pg.rep_n = rep_n;
-    pg.def = (const uint8_t*)def;
-    pg.def_n = def_n;
-    const int64_t n = pg.num_values;
-    if (n > 0) {
-      if (job.max_rep > 0 && rep_n >= 0)
-        reg_stream(job, streams, &pg.hs_rep, pidx, 0, rep, rep_n, bits_len((uint32_t)job.max_rep), n);
-      if (job.max_def > 0 && def_n >= 0)
-        reg_stream(job, streams, &pg.hs_def, pidx, 1, def, def_n, bits_len((uint32_t)job.max_def), n);
-    }
-    // values: RLE_DICTIONARY indices (first byte = bit width) / RLE booleans (u32 length)
-    const int64_t vn = blen - vpos;
-    gcu8 val = block + vpos;
-    if (pg.encoding == 8 && vn >= 1) {
-      const int w = val[0];
-      pg.dict_width = w;
-      if (w >= 1 && w <= 32 && n > 0) reg_stream(job, streams, &pg.hs_val, pidx, 2, val + 1, vn - 1, w, n);
-    } else if (pg.encoding == 3 && job.type == 0 && vn >= 4) {
-      const int64_t sz = rd_u32(val);
-      const int64_t take = min(sz, vn - 4);
-      if (n > 0) reg_stream(job, streams, &pg.hs_val, pidx, 3, val + 4, take, 1, n);
-    }
-    // value-stage page lists: 4-byte dictionary pages (the hot path, a kernel
-    // of its own), variable-length values (pqg_strings.hip) and everything else
-    const int mode = job.value_width == 0 ? 2 : (pg.encoding == 8 && job.value_width == 4) ? 1 : 0;
-    vlists[mode * list_cap + atomicAdd(&vcount[mode], 1)] = pidx;
-  }
 }
 
 // ---- K3b ---------------------------------------------------------------------
@@ -232,10 +135,11 @@ __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pag
                                                               HStream* streams, RunEnt* runs, BlockDesc* blks) {
   __shared__ uint32_t buf[32 * kWalkThreads];  // two 64-byte chunks per lane
   const int nt = *total;
-  for (int g = blockIdx.x * kWalkThreads + threadIdx.x; g < 3 * nt; g += gridDim.x * kWalkThreads) {
-    const int kind = g / nt;
-    const PageDev& pg = pages[list[g - kind * nt]];
-    const int hs = kind == 0 ? pg.hs_rep : kind == 1 ? pg.hs_def : pg.hs_val;
+  // level streams are decoded in place by k_page_levels: only the value streams
+  // (dictionary indices, RLE booleans) are walked
+  for (int g = blockIdx.x * kWalkThreads + threadIdx.x; g < nt; g += gridDim.x * kWalkThreads) {
+    const PageDev& pg = pages[list[g]];
+    const int hs = pg.hs_val;
     if (hs < 0) continue;
     HStream& S = streams[hs];
     const uint32_t w = (uint32_t)S.w;
@@ -369,74 +273,682 @@ __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pag
   }
 }
 
-// ---- K3c ---------------------------------------------------------------------
-struct LevelSink {
-  gu8 out;
-  uint32_t maxl;
-  int64_t nn;
-  __device__ __forceinline__ void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup],
-                                        const int (&cnt)[kGroup]) {
-#pragma unroll
-    for (int b = 0; b < kGroup; b++) {
-      if (cnt[b] == 0) continue;
-      gu8 o = out + i0[b];
-      if (cnt[b] == 8 && ((uintptr_t)o & 7) == 0) {
-        stg8((uintptr_t)o, v[b][0] | v[b][1] << 8 | v[b][2] << 16 | v[b][3] << 24,
-             v[b][4] | v[b][5] << 8 | v[b][6] << 16 | v[b][7] << 24);
-      } else {
-        for (int q = 0; q < cnt[b]; q++) o[q] = (uint8_t)v[b][q];
-      }
-      for (int q = 0; q < cnt[b]; q++) nn += v[b][q] == maxl;
+// ---- K3 fused: setup + level decode, one wave per data page -----------------
+//
+// The level streams (def/rep: bit widths 1..8) are run-dense (a run per ~10
+// slots at 10% nulls), so they are decoded where they are read, without run
+// tables: per window of 128 stream bytes (LDS),
+//   1. each lane parses a run header speculatively at two positions (lane,
+//      64 + lane): uvarint header, RLE value or bit-packed extent, errors;
+//   2. a scalar loop follows the true chain with v_readlane (a few cycles per
+//      run) and marks it;
+//   3. a DPP prefix sum gives each run its first value index; the runs up to
+//      the page's count (and <= kLSpan values, payload inside the window)
+//      form the batch; errors are checked lane-parallel, in stream order;
+//   4. each lane expands 16 consecutive values (its 16-byte output granule):
+//      its run by a prefix max over run marks, RLE -> the run value,
+//      bit-packed -> w bits of the staged payload; full granules are stored
+//      with one dwordx4, the batch's ragged ends byte by byte; notNull counts
+//      values == maxD.
+// A run longer than one batch (long RLE, wide bit-packed) goes in pieces.
+// Semantics are hybridDecoder.next (hybrid_decoder.go:82-166), exactly as the
+// walker: header EOF/overflow (> MaxInt32), empty runs, RLE value > w bits,
+// short bit-packed reads (the last needed group must start inside the
+// stream; bytes past it read as zero, Q5).
+constexpr int kLWin = 2048;   // stream window (LDS)
+constexpr int kLNeed = 1280;  // window bytes wanted at a batch's first run (headers + <= 1 KiB payload)
+constexpr int kLSpan = 1024;  // values per batch: 64 lanes x 16
+constexpr int kLPos = 128;    // header positions parsed per window
+
+struct LevShared {
+  uint8_t win[kLWin + 16];
+  uint32_t bm[kLSpan / 32 + 1];  // w == 1: the batch's values as a bitmap (bit j: value j from the granule base)
+  uint8_t tmap[kLSpan];  // 1 + run position at the run's first value (relative to the batch's granule base)
+  u32x2_t tent[kLPos];   // {first value (relative), BP: 0x80000000 | payload bit offset in the window; RLE: value}
+};
+
+__device__ __forceinline__ uint32_t ldpp_incl_add_sat(uint32_t x) {
+  // saturating 64-lane inclusive sum (row_shr 1/2/4/8, row_bcast 15/31)
+  uint32_t t;
+#define PQG_SAT_STEP(ctrl, rm, bc)                                                   \
+  t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, rm, 0xf, bc);           \
+  x = x + t < x ? 0xffffffffu : x + t;
+  PQG_SAT_STEP(0x111, 0xf, true) PQG_SAT_STEP(0x112, 0xf, true) PQG_SAT_STEP(0x114, 0xf, true)
+  PQG_SAT_STEP(0x118, 0xf, true) PQG_SAT_STEP(0x142, 0xa, false) PQG_SAT_STEP(0x143, 0xc, false)
+#undef PQG_SAT_STEP
+  return x;
+}
+__device__ __forceinline__ uint32_t ldpp_incl_max(uint32_t x) {
+  uint32_t t;
+#define PQG_MAX_STEP(ctrl, rm, bc)                                                   \
+  t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, rm, 0xf, bc);           \
+  x = t > x ? t : x;
+  PQG_MAX_STEP(0x111, 0xf, true) PQG_MAX_STEP(0x112, 0xf, true) PQG_MAX_STEP(0x114, 0xf, true)
+  PQG_MAX_STEP(0x118, 0xf, true) PQG_MAX_STEP(0x142, 0xa, false) PQG_MAX_STEP(0x143, 0xc, false)
+#undef PQG_MAX_STEP
+  return x;
+}
+
+// One speculative run header at stream position q (window bytes, zero past n).
+struct LRun {
+  uint32_t cnt;   // values the header declares (saturated)
+  uint32_t next;  // stream position of the next header (saturated)
+  uint32_t pay;   // BP: stream position of the payload; RLE: the value
+  int err;        // read error of the header / RLE value (kOK: none)
+  bool bp;
+  bool cplx;      // header longer than 4 bytes: resolved serially
+};
+
+__device__ __forceinline__ LRun parse_lrun(const PQG_L uint8_t* win, uint32_t wo, uint32_t q, uint32_t n, int w) {
+  const PQG_L uint32_t* d = (const PQG_L uint32_t*)(win + (wo & ~3u));
+  const uint32_t a = d[0], b = d[1], c = d[2];
+  const uint32_t sft = (wo & 3) * 8;
+  const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sft), hi = __builtin_amdgcn_alignbit(c, b, sft);
+  LRun r;
+  r.err = kOK;
+  r.cplx = false;
+  // readUVariant32 (helpers.go:149-165 via binary.ReadUvarint), 32-bit fast
+  // path for headers of <= 4 bytes (< 2^28: no MaxInt32 overflow); longer
+  // ones are walked serially.  Bytes past n read as zero (window fill), so a
+  // header running past the stream end terminates at or past n: EOF.
+  const uint32_t cont = ~lo & 0x80808080u;  // bytes without the continuation bit
+  const uint32_t hl = cont ? (uint32_t)(__builtin_ctz(cont) >> 3) + 1 : 5u;
+  uint32_t h = (lo & 0x7f) | ((lo >> 1) & 0x3f80) | ((lo >> 2) & 0x1fc000) | ((lo >> 3) & 0xfe00000);
+  h &= hl >= 4 ? 0xfffffffu : ((1u << (7 * hl)) - 1);
+  if (q >= n || (hl <= 4 && q + hl - 1 >= n)) r.err = kEOF;
+  else if (hl > 4) r.cplx = true;
+  r.bp = (h & 1) != 0;
+  const uint32_t g = h >> 1;
+  if (r.err == kOK && !r.cplx && g == 0) r.err = kRLE;  // empty run
+  if (r.bp) {
+    r.cnt = g * 8;  // g < 2^27
+    r.pay = q + hl;
+    const uint64_t nx = (uint64_t)q + hl + (uint64_t)g * (uint32_t)w;
+    r.next = nx > 0xffffffffull ? 0xffffffffu : (uint32_t)nx;
+  } else {
+    r.cnt = g;
+    const uint32_t vp = q + hl;  // rb = 1 byte for w <= 8
+    if (r.err == kOK && !r.cplx && vp >= n) r.err = kEOF;
+    r.pay = (hl < 4 ? (lo >> (8 * hl)) : hi) & 0xff;
+    if (r.err == kOK && !r.cplx && (r.pay >> w) != 0) r.err = kRLE;  // readRLERunValue :127-129
+    r.next = vp + 1;
+  }
+  return r;
+}
+
+// The exact header walk for one position (5+ byte varints): err, h, header length.
+__device__ int lrun_serial(const PQG_L uint8_t* win, uint32_t wo, uint32_t q, uint32_t n, uint32_t* h_out,
+                           uint32_t* hl_out) {
+  uint64_t v = 0;
+  unsigned sft = 0;
+  for (uint32_t i = 0;; i++) {
+    if (q + i >= n) return kEOF;
+    const uint32_t b = win[wo + i];
+    if (b < 0x80) {
+      if (i > 9 || (i == 9 && b > 1)) return kRLE;  // overflows uint64
+      v |= sft < 64 ? (uint64_t)b << sft : 0;
+      if (v > 0x7fffffffull) return kRLE;
+      *h_out = (uint32_t)v;
+      *hl_out = i + 1;
+      return kOK;
     }
+    if (sft < 64) v |= (uint64_t)(b & 0x7f) << sft;
+    sft += 7;
+  }
+}
+
+struct LevelDecoder {
+  gcu8 p;
+  uint32_t n;      // stream bytes
+  int w;           // bit width (1..8)
+  uint32_t count;  // values wanted
+  gu8 out;         // count bytes
+  uint32_t maxl;
+  LevShared* sh;
+  uint32_t wbase = 0;  // stream offset of win[0] (16-aligned in memory, may precede the stream)
+  bool have = false;
+  uint32_t nn = 0;     // per lane: values == maxl
+#ifdef PQG_PROFILE
+  uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per-wave phase cycles / counts (one atomic per stream)
+#define PQG_LT(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define PQG_LA(k, x) pacc[k] += (x)
+#else
+#define PQG_LT(v)
+#define PQG_LA(k, x)
+#endif
+
+  __device__ void fill(uint32_t at) {
+    const int lane = lane_id();
+    const uint32_t mis = (uint32_t)((uintptr_t)(p + at) & 15);
+    wbase = at - mis;  // wraps below 0 for the first window of a misaligned stream: offsets are modular
+    have = true;
+    uint4 v[kLWin / 1024];
+#pragma unroll
+    for (int h = 0; h < kLWin / 1024; h++) {
+      const int64_t g = (int64_t)at - mis + 1024 * h + 16 * lane;
+      // granules holding a stream byte are mapped; bytes past n read as zero (Q5)
+      v[h] = (g < (int64_t)n && g + 16 > 0) ? mask_tail(ldg16((uintptr_t)(p + g)), g, n) : make_uint4(0, 0, 0, 0);
+      if (g < 0 && g + 16 > 0) {  // bytes before the stream start: zero too (never read as data)
+        uint32_t ww[4] = {v[h].x, v[h].y, v[h].z, v[h].w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int64_t b = g + 4 * k;
+          if (b + 4 <= 0) ww[k] = 0;
+          else if (b < 0) ww[k] &= 0xffffffffu << (8 * (int)(-b));
+        }
+        v[h] = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int h = 0; h < kLWin / 1024; h++) sts16(lds_ptr(sh->win) + 1024 * h + 16 * lane, v[h]);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ __forceinline__ bool in_win(uint32_t a, uint32_t len) const {
+    return have && a - wbase <= (uint32_t)kLWin && a - wbase + len <= (uint32_t)kLWin;
+  }
+
+  // Expand values [v0, v0 + cnt) of the page (cnt <= kLSpan - pre), given the
+  // run tables; stores the granules and counts notNull.
+  __device__ void expand(uint32_t v0, uint32_t cnt) {
+    const int lane = lane_id();
+    const uintptr_t oa = (uintptr_t)(out + v0);
+    const uintptr_t a0 = oa & ~(uintptr_t)15;
+    const int pre = (int)(oa - a0);
+    const int end = pre + (int)cnt;
+    const u32x4_t mk = *(const PQG_L u32x4_t*)(lds_ptr(sh->tmap) + 16 * lane);
+    const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
+    uint32_t tix[16];
+    uint32_t run_max = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t m = (mw[k >> 2] >> (8 * (k & 3))) & 0xff;
+      run_max = m > run_max ? m : run_max;
+      tix[k] = run_max;
+    }
+    uint32_t before = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ldpp_incl_max(run_max), 0x138, 0xf, 0xf, false);
+    const PQG_L u32x2_t* TE = lds_ptr(sh->tent);
+    const PQG_L uint8_t* W = lds_ptr(sh->win);
+    const uint32_t mask = (1u << w) - 1;
+    uint32_t val[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t t = (tix[k] > before ? tix[k] : before);
+      const u32x2_t te = TE[(t - 1) & (kLPos - 1)];  // t >= 1 for every value of the batch
+      const uint32_t rel = (uint32_t)(16 * lane + k) - te.x;
+      const bool bp = (te.y & 0x80000000u) != 0;
+      const uint32_t bit = bp ? (te.y & 0x7fffffffu) + rel * (uint32_t)w : 0u;
+      const PQG_L uint32_t* dw = (const PQG_L uint32_t*)(W + ((bit >> 3) & ~3u));
+      const uint32_t lo = dw[0], hi = dw[1];
+      const uint32_t bits = __builtin_amdgcn_alignbit(hi, lo, bit & 31) & mask;
+      val[k] = bp ? bits : te.y;
+    }
+    uint32_t wv[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) wv[k] = val[4 * k] | val[4 * k + 1] << 8 | val[4 * k + 2] << 16 | val[4 * k + 3] << 24;
+    const int i0 = 16 * lane;
+    if (i0 >= pre && i0 + 16 <= end) {
+      stg16(a0 + i0, make_uint4(wv[0], wv[1], wv[2], wv[3]));
+#pragma unroll
+      for (int k = 0; k < 16; k++) nn += val[k] == maxl;
+    } else if (i0 + 16 > pre && i0 < end) {
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        if (i0 + k >= pre && i0 + k < end) {
+          *(PQG_G uint8_t*)(a0 + i0 + k) = (uint8_t)val[k];
+          nn += val[k] == maxl;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // ---- w == 1 (maxLevel 1, the common optional / single-list case): values
+  // are bits.  Each run ORs its bits into an LDS bitmap, one dword at a time
+  // (RLE: ones or nothing; bit-packed: 32 payload bits via alignbit); each
+  // lane then spreads its 16 bits into 16 level bytes (nibble x 0x00204081)
+  // and counts notNull with one popcount.
+  __device__ __forceinline__ void bits_or(uint32_t st, uint32_t len, bool bp, uint32_t info, uint32_t k) {
+    const uint32_t lo = st > 32 * k ? st : 32 * k;
+    const uint32_t e = st + len, hi = e < 32 * k + 32 ? e : 32 * k + 32;
+    if (lo >= hi) return;
+    const uint32_t cnt = hi - lo;
+    const uint32_t m = cnt >= 32 ? 0xffffffffu : ((1u << cnt) - 1);
+    uint32_t v;
+    if (bp) {
+      const uint32_t sb = info + (lo - st);  // payload bit in the window
+      const PQG_L uint32_t* W = (const PQG_L uint32_t*)lds_ptr(sh->win);
+      v = __builtin_amdgcn_alignbit(W[(sb >> 5) + 1], W[sb >> 5], sb & 31) & m;
+    } else {
+      v = info ? m : 0u;
+    }
+    v <<= (lo - 32 * k);
+    if (v) __hip_atomic_fetch_or(&sh->bm[k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  }
+  __device__ __forceinline__ void bits_clear() {
+    const int lane = lane_id();
+    if (lane <= kLSpan / 32) lds_ptr(sh->bm)[lane] = 0u;
+    __builtin_amdgcn_wave_barrier();
+  }
+  // store values [v0, v0 + cnt) from the bitmap (granule base = out + v0 rounded down to 16)
+  __device__ void bits_store(uint32_t v0, uint32_t cnt) {
+    const int lane = lane_id();
+    __builtin_amdgcn_wave_barrier();
+    const uintptr_t oa = (uintptr_t)(out + v0);
+    const uintptr_t a0 = oa & ~(uintptr_t)15;
+    const int pre = (int)(oa - a0);
+    const int end = pre + (int)cnt;
+    const uint32_t b16 = (lds_ptr(sh->bm)[lane >> 1] >> ((lane & 1) * 16)) & 0xffffu;
+    uint32_t wv[4];
+#pragma unroll
+    for (int g = 0; g < 4; g++) wv[g] = (((b16 >> (4 * g)) & 0xfu) * 0x00204081u) & 0x01010101u;
+    const int i0 = 16 * lane;
+    if (i0 >= pre && i0 + 16 <= end) {
+      stg16(a0 + i0, make_uint4(wv[0], wv[1], wv[2], wv[3]));
+      if (maxl == 1) nn += __builtin_popcount(b16);
+    } else if (i0 + 16 > pre && i0 < end) {
+      uint32_t vm = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        if (i0 + k >= pre && i0 + k < end) {
+          *(PQG_G uint8_t*)(a0 + i0 + k) = (uint8_t)((b16 >> k) & 1);
+          vm |= 1u << k;
+        }
+      }
+      if (maxl == 1) nn += __builtin_popcount(b16 & vm);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // decode `count` values; kOK or the stream's first error
+  __device__ int run() {
+    const int lane = lane_id();
+    uint32_t pos = 0, produced = 0;
+    const uintptr_t oa0 = (uintptr_t)out;
+    while (produced < count) {
+      if (pos >= n) return kEOF;
+      PQG_LT(ta);
+      if (!in_win(pos, kLNeed)) {
+        fill(pos);
+        PQG_LA(6, 1);
+      }
+      PQG_LT(tb);
+      PQG_LA(0, tb - ta);
+      const uint32_t wo = pos - wbase;
+      const uint32_t pre = (uint32_t)((oa0 + produced) & 15);
+      const uint32_t left = count - produced;
+      // ---- 1. speculative headers
+      const LRun r0 = parse_lrun(lds_ptr(sh->win), wo + lane, pos + lane, n, w);
+      const LRun r1 = parse_lrun(lds_ptr(sh->win), wo + 64 + lane, pos + 64 + lane, n, w);
+      auto nxt = [&](const LRun& r, uint32_t rel) -> int {
+        if (r.err != kOK || r.cplx) return kLPos;
+        const uint32_t d = r.next - pos;  // > rel
+        return d < (uint32_t)kLPos ? (int)d : kLPos;
+      };
+      const int n0 = nxt(r0, lane), n1 = nxt(r1, 64 + lane);
+      // ---- 2. the chain
+      uint64_t cm0 = 0, cm1 = 0;
+      int pp = 0;
+      while (pp < kLPos) {
+        const int l = pp & 63;
+        const int a = __builtin_amdgcn_readlane(n0, l), b = __builtin_amdgcn_readlane(n1, l);
+        if (pp < 64) { cm0 |= 1ull << l; pp = a; }
+        else { cm1 |= 1ull << l; pp = b; }
+      }
+      const bool on0 = (cm0 >> lane) & 1, on1 = (cm1 >> lane) & 1;
+      PQG_LT(tc);
+      PQG_LA(1, tc - tb);
+      // ---- 3. value offsets, takes, checks
+      const uint32_t c0 = on0 ? r0.cnt : 0u, c1 = on1 ? r1.cnt : 0u;
+      const uint32_t i0 = ldpp_incl_add_sat(c0);
+      const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)i0, 63);
+      uint32_t i1 = ldpp_incl_add_sat(c1);
+      i1 = i1 + t0 < i1 ? 0xffffffffu : i1 + t0;
+      const uint32_t s0 = i0 - c0, s1 = i1 - c1;  // values before the run (within this window)
+      // a run is needed while values before it < left; its take is min(cnt, left - before)
+      auto assess = [&](const LRun& r, uint32_t st, bool on, int& e, uint32_t& take, bool& cut) {
+        e = kOK;
+        take = 0;
+        cut = false;
+        if (!on || st >= left) return;
+        if (r.cplx) { e = kCOMPLEX; return; }
+        if (r.err != kOK) { e = r.err; return; }
+        take = r.cnt < left - st ? r.cnt : left - st;
+        if (r.bp) {
+          const uint64_t need = (take + 7) >> 3;
+          if ((uint64_t)r.pay + (need - 1) * (uint32_t)w >= n) {  // short read: whole groups that start in the stream
+            const uint32_t ok = r.pay < n ? (n - r.pay + (uint32_t)w - 1) / (uint32_t)w : 0u;
+            take = ok * 8;
+            e = kEOF;
+          }
+          const uint64_t pend = (uint64_t)r.pay + (((uint64_t)take * (uint32_t)w + 7) >> 3) + 8;
+          cut = !in_win(r.pay, (uint32_t)(pend - r.pay));
+        }
+        cut |= pre + st + take > (uint32_t)kLSpan;
+      };
+      int e0, e1;
+      uint32_t k0, k1;
+      bool x0, x1;
+      assess(r0, s0, on0, e0, k0, x0);
+      assess(r1, s1, on1, e1, k1, x1);
+      const uint64_t eb0 = __ballot(e0 != kOK), eb1 = __ballot(e1 != kOK);
+      const uint64_t xb0 = __ballot(x0), xb1 = __ballot(x1);
+      const uint64_t nb0 = __ballot(on0 && s0 < left), nb1 = __ballot(on1 && s1 < left);  // needed runs
+      const int first_err = eb0 ? __ffsll((long long)eb0) - 1 : eb1 ? 64 + __ffsll((long long)eb1) - 1 : kLPos;
+      const int first_cut = xb0 ? __ffsll((long long)xb0) - 1 : xb1 ? 64 + __ffsll((long long)xb1) - 1 : kLPos;
+      PQG_LT(td);
+      PQG_LA(2, td - tc);
+      if (first_err < first_cut) {
+        // runs before the error are fine: the stream fails there (for levels the
+        // values do not matter then); a 5+ byte header is walked serially
+        const int l = first_err & 63;
+        const int e = __builtin_amdgcn_readlane(first_err < 64 ? e0 : e1, l);
+        if (e != kCOMPLEX) return e;
+        // serial header at the complex run, then that single run as a long run
+        const uint32_t q = pos + (uint32_t)first_err;
+        // produce the runs before it first
+        const uint32_t before_v = (uint32_t)__builtin_amdgcn_readlane((int)(first_err < 64 ? s0 : s1), l);
+        if (first_err > 0) {
+          const int ee = emit_batch(cm0, cm1, first_err, r0, r1, s0, s1, k0, k1, produced, before_v);
+          if (ee) return ee;
+        }
+        produced += before_v;
+        uint32_t h, hl;
+        const int es = lrun_serial(lds_ptr(sh->win), q - wbase, q, n, &h, &hl);
+        if (es) return es;
+        if ((h >> 1) == 0) return kRLE;
+        const int el = long_run(q, h, hl, produced, pos);
+        if (el) return el;
+        continue;
+      }
+      if (first_cut == 0) {
+        // run 0 alone is longer than a batch (or its payload leaves the window)
+        uint32_t h;  // rebuild the header fields of run 0
+        const bool bp = __builtin_amdgcn_readlane((int)r0.bp, 0) != 0;
+        const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane((int)r0.cnt, 0);
+        const uint32_t pay = (uint32_t)__builtin_amdgcn_readlane((int)r0.pay, 0);
+        const uint32_t nx = (uint32_t)__builtin_amdgcn_readlane((int)r0.next, 0);
+        const int el = long_run_fields(bp, cnt, pay, nx, produced, pos);
+        PQG_LA(7, 1);
+        (void)h;
+        if (el) return el;
+        continue;
+      }
+      // ---- 4. the batch: needed runs before the cut
+      const int nruns = first_cut;  // positions < nruns
+      const uint64_t need0 = nb0, need1 = nb1;
+      const int e = emit_batch(cm0 & need0, cm1 & need1, nruns, r0, r1, s0, s1, k0, k1, produced, 0xffffffffu);
+      if (e) return e;
+      // values and the next header position: from the last batch run
+      const uint64_t bm0 = cm0 & need0 & (nruns >= 64 ? ~0ull : ((1ull << nruns) - 1));
+      const uint64_t bm1 = nruns > 64 ? cm1 & need1 & (nruns >= 128 ? ~0ull : ((1ull << (nruns - 64)) - 1)) : 0ull;
+      const bool last_hi = bm1 != 0;
+      const int ll = 63 - __builtin_clzll(last_hi ? bm1 : bm0);
+      const uint32_t lst = (uint32_t)__builtin_amdgcn_readlane((int)(last_hi ? s1 : s0), ll);
+      const uint32_t ltk = (uint32_t)__builtin_amdgcn_readlane((int)(last_hi ? k1 : k0), ll);
+      const uint32_t lnx = (uint32_t)__builtin_amdgcn_readlane((int)(last_hi ? r1.next : r0.next), ll);
+      produced += lst + ltk;
+      pos = lnx;
+      PQG_LT(te);
+      PQG_LA(3, te - td);
+      PQG_LA(4, 1);
+      PQG_LA(5, __popcll(bm0) + __popcll(bm1));
+    }
+    return kOK;
+  }
+
+  // Run tables + expansion for the chain's runs at positions < nruns (masks
+  // m0/m1), values [produced, produced + total).  A run's value limit is its take.
+  __device__ int emit_batch(uint64_t m0, uint64_t m1, int nruns, const LRun& r0, const LRun& r1, uint32_t s0,
+                            uint32_t s1, uint32_t k0, uint32_t k1, uint32_t produced, uint32_t limit) {
+    const int lane = lane_id();
+    const uint64_t lm0 = nruns >= 64 ? ~0ull : ((1ull << nruns) - 1);
+    const uint64_t lm1 = nruns > 64 ? (nruns >= 128 ? ~0ull : ((1ull << (nruns - 64)) - 1)) : 0ull;
+    m0 &= lm0;
+    m1 &= lm1;
+    const bool b0 = (m0 >> lane) & 1, b1 = (m1 >> lane) & 1;
+    const uint32_t pre = (uint32_t)(((uintptr_t)out + produced) & 15);
+    if (w == 1) {
+      bits_clear();
+      const bool hi = m1 != 0;
+      const int ll = 63 - __builtin_clzll(hi ? m1 : m0);
+      uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(hi ? s1 : s0), ll) +
+                       (uint32_t)__builtin_amdgcn_readlane((int)(hi ? k1 : k0), ll);
+      if (total > limit) total = limit;
+      // each run lane ORs the dwords its values cover
+      const uint32_t st0 = pre + s0, st1 = pre + s1;
+      const uint32_t l0 = b0 ? (k0 < total - s0 ? k0 : total - s0) : 0u;
+      const uint32_t l1 = b1 ? (s1 < total ? (k1 < total - s1 ? k1 : total - s1) : 0u) : 0u;
+      const uint32_t inf0 = r0.bp ? (r0.pay - wbase) * 8 : r0.pay, inf1 = r1.bp ? (r1.pay - wbase) * 8 : r1.pay;
+      if (l0) for (uint32_t k = st0 >> 5; k <= (st0 + l0 - 1) >> 5; k++) bits_or(st0, l0, r0.bp, inf0, k);
+      if (l1) for (uint32_t k = st1 >> 5; k <= (st1 + l1 - 1) >> 5; k++) bits_or(st1, l1, r1.bp, inf1, k);
+      if (total) bits_store(produced, total);
+      return kOK;
+    }
+    PQG_L uint8_t* TM = lds_ptr(sh->tmap);
+    PQG_L u32x2_t* TE = lds_ptr(sh->tent);
+    *(PQG_L u32x4_t*)(TM + 16 * lane) = u32x4_t{0u, 0u, 0u, 0u};
+    __builtin_amdgcn_wave_barrier();
+    if (b0) {
+      TE[lane] = u32x2_t{pre + s0, r0.bp ? (0x80000000u | ((r0.pay - wbase) * 8)) : r0.pay};
+      TM[pre + s0] = (uint8_t)(lane + 1);
+    }
+    if (b1) {
+      TE[64 + lane] = u32x2_t{pre + s1, r1.bp ? (0x80000000u | ((r1.pay - wbase) * 8)) : r1.pay};
+      TM[pre + s1] = (uint8_t)(65 + lane);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // total values: the last run's start + take
+    const bool hi = m1 != 0;
+    const int ll = 63 - __builtin_clzll(hi ? m1 : m0);
+    uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(hi ? s1 : s0), ll) +
+                     (uint32_t)__builtin_amdgcn_readlane((int)(hi ? k1 : k0), ll);
+    if (total > limit) total = limit;
+    if (total) expand(produced, total);
+    return kOK;
+  }
+
+  // One run [header at q] in pieces of <= kLSpan values.
+  __device__ int long_run(uint32_t q, uint32_t h, uint32_t hl, uint32_t& produced, uint32_t& pos) {
+    const bool bp = (h & 1) != 0;
+    const uint32_t g = h >> 1;
+    uint32_t cnt, pay, nx;
+    if (bp) {
+      cnt = g > 0x1fffffffu ? 0xffffffffu : g * 8;
+      pay = q + hl;
+      const uint64_t t = (uint64_t)q + hl + (uint64_t)g * (uint32_t)w;
+      nx = t > 0xffffffffull ? 0xffffffffu : (uint32_t)t;
+    } else {
+      const uint32_t vp = q + hl;
+      if (vp >= n) return kEOF;
+      if (!in_win(vp, 1)) fill(vp);
+      pay = lds_ptr(sh->win)[vp - wbase];
+      if ((pay >> w) != 0) return kRLE;
+      cnt = g;
+      nx = vp + 1;
+    }
+    return long_run_fields(bp, cnt, pay, nx, produced, pos);
+  }
+
+  __device__ int long_run_fields(bool bp, uint32_t cnt, uint32_t pay, uint32_t nx, uint32_t& produced, uint32_t& pos) {
+    const int lane = lane_id();
+    const uint32_t left = count - produced;
+    uint32_t take = cnt < left ? cnt : left;
+    int status = kOK;
+    if (bp) {
+      const uint64_t need = (take + 7) >> 3;
+      if ((uint64_t)pay + (need - 1) * (uint32_t)w >= n) {
+        const uint32_t ok = pay < n ? (n - pay + (uint32_t)w - 1) / (uint32_t)w : 0u;
+        take = ok * 8;
+        status = kEOF;
+      }
+    }
+    if (status != kOK) return status;  // levels: the values of a failing stream do not matter
+    uint32_t done = 0;
+    while (done < take) {
+      const uint32_t pre = (uint32_t)(((uintptr_t)out + produced) & 15);
+      uint32_t piece = take - done;
+      if (piece > (uint32_t)kLSpan - pre) piece = (uint32_t)kLSpan - pre;
+      uint32_t info = pay;
+      if (bp) {
+        const uint64_t b0 = (uint64_t)pay * 8 + (uint64_t)done * (uint32_t)w;  // stream bit of the piece
+        const uint32_t byte0 = (uint32_t)(b0 >> 3);
+        const uint32_t nbytes = (uint32_t)(((uint64_t)piece * (uint32_t)w + 7) >> 3) + 8;
+        if (!in_win(byte0, nbytes)) fill(byte0);
+        info = 0x80000000u | (uint32_t)(((uint64_t)(byte0 - wbase) << 3) + (b0 & 7));
+      }
+      if (w == 1) {
+        // one dword of the piece per lane
+        bits_clear();
+        if ((uint32_t)lane <= (pre + piece - 1) >> 5) bits_or(pre, piece, bp, bp ? (info & 0x7fffffffu) : pay, lane);
+        bits_store(produced, piece);
+        produced += piece;
+        done += piece;
+        continue;
+      }
+      PQG_L uint8_t* TM = lds_ptr(sh->tmap);
+      *(PQG_L u32x4_t*)(TM + 16 * lane) = u32x4_t{0u, 0u, 0u, 0u};
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) {
+        lds_ptr(sh->tent)[0] = u32x2_t{pre, info};
+        TM[pre] = 1;
+      }
+      __builtin_amdgcn_wave_barrier();
+      expand(produced, piece);
+      produced += piece;
+      done += piece;
+    }
+    pos = nx;
+    return kOK;
   }
 };
 
-__global__ void __launch_bounds__(64) k_levels_expand(JobDev* jobs, PageDev* pages, const int* list,
-                                                      const int* total, int* queue, const HStream* streams,
-                                                      const RunEnt* runs, const BlockDesc* blks, uint8_t* def_arena,
-                                                      uint8_t* rep_arena) {
-  __shared__ __attribute__((aligned(16))) ExpandShared sh;
+__device__ __forceinline__ int level_stream(gcu8 p, int64_t n, int w, uint32_t count, gu8 out, uint32_t maxl,
+                                            LevShared& sh, uint32_t* nn) {
+  LevelDecoder dec{p, (uint32_t)n, w, count, out, maxl, &sh};
+  const int e = dec.run();
+#ifdef PQG_PROFILE
+  for (int k = 0; k < 8; k++) PQG_ACC(k, 0, dec.pacc[k]);
+#endif
+  *nn = (uint32_t)wave_sum((int64_t)dec.nn);
+  return e;
+}
+
+// Setup (the read phase of the page, as k_page_setup) and the level decode
+// (as k_levels_expand) of one data page per wave; the value streams are
+// registered for the walker.
+__global__ void __launch_bounds__(64) k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+                                                    int* queue, uint8_t* scratch, HStream* streams, int* vlists,
+                                                    int* vcount, int list_cap, uint8_t* def_arena,
+                                                    uint8_t* rep_arena) {
+  __shared__ __attribute__((aligned(16))) LevShared sh;
   const int lane = lane_id();
   for (;;) {
     const int t = queue_next(queue);
     if (t >= *total) return;
-    // wave-uniform index: the page / job / stream records below are read once
-    // with scalar loads into locals; read through references, every output
-    // store (which might alias them) would force a re-load and a vmcnt wait
     const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
     const PageDev pg = pages[pidx];
+    if (lane == 0) pages[pidx].hs_rep = pages[pidx].hs_def = pages[pidx].hs_val = -1;
     if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3)) continue;
     const JobDev job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
-    // readValues (page_v1.go:27-55): rep levels, then def levels, then values
+    // ---- the page block and its level / value streams (read phase)
+    gcu8 block;
+    int64_t blen;
+    int32_t levels = 0;
+    if (pg.page_type == 3) {
+      levels = (int32_t)((uint32_t)pg.rep_len + (uint32_t)pg.def_len);
+      blen = (int32_t)((uint32_t)pg.csize - (uint32_t)levels);
+      if (pg.scratch_offset >= 0) blen = (int32_t)((uint32_t)pg.usize - (uint32_t)levels);
+    } else {
+      blen = pg.scratch_offset >= 0 ? pg.usize : pg.csize;
+    }
+    if (pg.scratch_offset >= 0) block = gconst(scratch) + job.scratch_base + pg.scratch_offset;
+    else block = gconst(job.data) + pg.payload_offset + (levels > 0 ? levels : 0);
+    gcu8 rep = nullptr, def = nullptr;
+    int64_t rep_n = -1, def_n = -1;  // -1: the level decoder is not initialised
+    int64_t vpos = 0;
+    int e = kOK;
+    if (pg.page_type == 0) {
+      // rDecoder.initSize then dDecoder.initSize (page_v1.go:99-105)
+      if (job.max_rep > 0) {
+        if (blen - vpos < 4) e = kEOF;
+        else {
+          const int64_t sz = rd_u32(block + vpos);
+          const int64_t take = min(sz, blen - vpos - 4);
+          rep = block + vpos + 4;
+          rep_n = take;
+          vpos += 4 + take;
+        }
+      }
+      if (e == kOK && job.max_def > 0) {
+        if (blen - vpos < 4) e = kEOF;
+        else {
+          const int64_t sz = rd_u32(block + vpos);
+          const int64_t take = min(sz, blen - vpos - 4);
+          def = block + vpos + 4;
+          def_n = take;
+          vpos += 4 + take;
+        }
+      }
+    } else {
+      // V2: raw level bytes, a decoder only for a non-empty section (page_v2.go:110-120)
+      gcu8 lv = gconst(job.data) + pg.payload_offset;
+      if (levels > 0 && pg.rep_len > 0) { rep = lv; rep_n = pg.rep_len; }
+      if (levels > 0 && pg.def_len > 0) { def = lv + pg.rep_len; def_n = levels - pg.rep_len; }
+    }
+    if (e != kOK) {
+      if (lane == 0) pages[pidx].read_status = e;
+      continue;
+    }
     const int64_t n = pg.num_values;
+    const int64_t vn = blen - vpos;
+    gcu8 val = block + vpos;
+    if (lane == 0) {
+      PageDev& P = pages[pidx];
+      P.block = (const uint8_t*)block;
+      P.block_len = blen;
+      P.val = (const uint8_t*)val;
+      P.val_n = vn;
+      P.rep = (const uint8_t*)rep;
+      P.rep_n = rep_n;
+      P.def = (const uint8_t*)def;
+      P.def_n = def_n;
+      // values: RLE_DICTIONARY indices (first byte = bit width) / RLE booleans (u32 length)
+      if (pg.encoding == 8 && vn >= 1) {
+        const int wv = val[0];
+        P.dict_width = wv;
+        if (wv >= 1 && wv <= 32 && n > 0) reg_stream(jobs[pg.job], streams, &P.hs_val, pidx, 2, val + 1, vn - 1, wv, n);
+      } else if (pg.encoding == 3 && job.type == 0 && vn >= 4) {
+        const int64_t sz = rd_u32(val);
+        const int64_t take = min(sz, vn - 4);
+        if (n > 0) reg_stream(jobs[pg.job], streams, &P.hs_val, pidx, 3, val + 4, take, 1, n);
+      }
+      // value-stage page lists: 4-byte dictionary pages (the hot path, a kernel
+      // of its own), variable-length values (pqg_strings.hip) and everything else
+      const int mode = job.value_width == 0 ? 2 : (pg.encoding == 8 && job.value_width == 4) ? 1 : 0;
+      vlists[mode * list_cap + atomicAdd(&vcount[mode], 1)] = pidx;
+    }
+    // ---- readValues (page_v1.go:27-55): rep levels, then def levels
     int64_t nn = 0;
     int de = kOK;
     if (n > 0) {
       if (job.max_rep > 0) {
-        if (pg.rep_n < 0) {
-          de = kLEVELS;  // V2 with no rep-level bytes: "reader is not initialized"
-        } else {
-          const HStream S = streams[pg.hs_rep];
-          if (S.status != kOK) de = S.status;
-          else {
-            LevelSink sk{gmut(rep_arena) + job.slot_base + pg.slot_offset, (uint32_t)job.max_rep, 0};
-            hybrid_expand(S, runs, blks, n, sh, sk);
-          }
+        if (rep_n < 0) de = kLEVELS;  // V2 with no rep-level bytes: "reader is not initialized"
+        else {
+          uint32_t unused;
+          de = level_stream(rep, rep_n, bits_len((uint32_t)job.max_rep), (uint32_t)n,
+                            gmut(rep_arena) + job.slot_base + pg.slot_offset, 0x100u, sh, &unused);
         }
       }
       if (de == kOK) {
         if (job.max_def > 0) {
-          if (pg.def_n < 0) {
-            de = kLEVELS;
-          } else {
-            const HStream S = streams[pg.hs_def];
-            if (S.status != kOK) de = S.status;
-            else {
-              LevelSink sk{gmut(def_arena) + job.slot_base + pg.slot_offset, (uint32_t)job.max_def, 0};
-              hybrid_expand(S, runs, blks, n, sh, sk);
-              nn = wave_sum(sk.nn);
-            }
+          if (def_n < 0) de = kLEVELS;
+          else {
+            uint32_t c;
+            de = level_stream(def, def_n, bits_len((uint32_t)job.max_def), (uint32_t)n,
+                              gmut(def_arena) + job.slot_base + pg.slot_offset, (uint32_t)job.max_def, sh, &c);
+            nn = c;
           }
         } else {
           nn = n;
@@ -444,7 +956,7 @@ __global__ void __launch_bounds__(64) k_levels_expand(JobDev* jobs, PageDev* pag
       }
     }
     if (lane == 0) {
-      pages[pidx].not_null = (int32_t)nn;
+      pages[pidx].not_null = de == kOK ? (int32_t)nn : 0;
       if (de != kOK) pages[pidx].decode_status = de;
     }
   }

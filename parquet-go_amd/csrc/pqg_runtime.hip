@@ -39,13 +39,11 @@ __global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs);
 __global__ void k_page_list(JobDev* jobs, int n_jobs, int* list, int list_cap, int* total, int* queues);
 __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                          uint8_t* scratch);
-__global__ void k_page_setup(JobDev* jobs, PageDev* pages, const int* list, const int* total, uint8_t* scratch,
-                             HStream* streams, int* vlists, int* vcount, int list_cap);
+__global__ void k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                              uint8_t* scratch, HStream* streams, int* vlists, int* vcount, int list_cap,
+                              uint8_t* def_arena, uint8_t* rep_arena);
 __global__ void k_hybrid_walk(const PageDev* pages, const int* list, const int* total, HStream* streams,
                               RunEnt* runs, BlockDesc* blks);
-__global__ void k_levels_expand(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
-                                const HStream* streams, const RunEnt* runs, const BlockDesc* blks, uint8_t* def_arena,
-                                uint8_t* rep_arena);
 __global__ void k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch);
 template <int Mode>
 __global__ void k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
@@ -405,18 +403,16 @@ static int launch_pipeline(pqg_ctx* c) {
   HStream* streams = (HStream*)c->streams.p;
   RunEnt* runs = (RunEnt*)c->runs.p;
   BlockDesc* blks = (BlockDesc*)c->blks.p;
-  const unsigned lane_blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((c->list_cap + 255) / 256, c->num_cus * 4));
   int* vlists = (int*)c->vlists.p;
   const int lcap = (int)std::min<int64_t>(c->list_cap, INT32_MAX);
-  hipLaunchKernelGGL(k_page_setup, dim3(lane_blocks), dim3(256), 0, s, jobs, pages, list, ctr, scratch, streams, vlists,
-                     ctr + 12, lcap);
+  // setup + def/rep levels, one wave per data page (value streams registered for the walk)
+  hipLaunchKernelGGL(k_page_levels, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 9, scratch, streams,
+                     vlists, ctr + 12, lcap, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p);
   if (c->timed) hipEventRecord(c->ev[4], s);
   const unsigned walk_blocks =
-      (unsigned)std::max<int64_t>(1, std::min<int64_t>((3 * c->list_cap + 255) / 256, c->num_cus * 8));
+      (unsigned)std::max<int64_t>(1, std::min<int64_t>((c->list_cap + 255) / 256, c->num_cus * 8));
   hipLaunchKernelGGL(k_hybrid_walk, dim3(walk_blocks), dim3(256), 0, s, pages, list, ctr, streams, runs, blks);
   if (c->timed) hipEventRecord(c->ev[5], s);
-  hipLaunchKernelGGL(k_levels_expand, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 9, streams, runs, blks,
-                     (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p);
   if (c->timed) hipEventRecord(c->ev[6], s);
   hipLaunchKernelGGL(k_nn_scan, dim3(n), dim3(256), 0, s, jobs, pages, scratch);
   if (c->timed) hipEventRecord(c->ev[7], s);
