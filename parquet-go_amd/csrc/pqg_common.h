@@ -69,7 +69,8 @@ struct PageDev {
   int32_t flags;
   int32_t dict_width;      // RLE_DICTIONARY: index bit width byte
   int32_t hs_rep, hs_def, hs_val;  // hybrid streams of the page (HStream index, -1: none)
-  int32_t pad;
+  int32_t vmode;           // values stage of the page: 1 4-byte dictionary, 0 other fixed width, 2 variable, -1 none
+  int64_t run_off, blk_off;  // the page's run-table / block-index region (job-relative, k_page_list)
   // variable-length values (BYTE_ARRAY, FLBA of length 0): chars of the page
   // and their offset in the chunk's chars (exclusive scan over the pages)
   int64_t chars;
@@ -154,8 +155,13 @@ struct JobDev {
   // ---- K3 hybrid run tables (pqg_levels.hip)
   int64_t run_cap, run_base;   // RunEnt arena region
   int64_t blk_cap, blk_base;   // block-index arena region
-  int64_t run_used, blk_used;  // bump allocators (zeroed by the scan)
+  int64_t run_used, blk_used;  // run-table / block-index entries the pages need (k_page_list)
 };
+
+// Work queues: kQShards heads kQStride ints apart (see queue_pull, pqg_device.h).
+constexpr int kQShards = 8;
+constexpr int kQStride = 32;
+constexpr int kQueueInts = kQShards * kQStride;
 
 // Scan tiles of the speculative page-header search.
 constexpr int kScanTile = 16384;

@@ -203,12 +203,22 @@ static __device__ unsigned long long pqg_prof[64];  // one per translation unit 
 #define PQG_ACC(slot, a, b) do { } while (0)
 #endif
 
-// Next item of an atomic work queue, wave-uniform (in an SGPR): struct loads
-// indexed by it become scalar loads, which do not queue behind vector loads
-// and stores (vmcnt) the way vector loads of the same fields would.
+// Work queues are sharded over the 8 XCDs: one device-scope atomic word
+// saturates near 88 dequeues/us (MI355X_MICROARCH.md, dequeue row), i.e.
+// ~0.4 ms for 35 000 pages.  Blocks are dealt round-robin over the XCDs, so
+// shard = blockIdx & 7 keeps each head on one XCD; shard s hands out items
+// s, s + 8, s + 16, ...  A queue is kQShards heads kQStride ints apart (one
+// 128-byte line each), zeroed before the launch.
+__device__ __forceinline__ int queue_pull(int* queue) {
+  const int shard = (int)(blockIdx.x & (kQShards - 1));
+  return atomicAdd(queue + shard * kQStride, 1) * kQShards + shard;
+}
+// Next item, wave-uniform (in an SGPR): struct loads indexed by it become
+// scalar loads, which do not queue behind vector loads and stores (vmcnt) the
+// way vector loads of the same fields would.
 __device__ __forceinline__ int queue_next(int* queue) {
   int t = 0;
-  if (lane_id() == 0) t = atomicAdd(queue, 1);
+  if (lane_id() == 0) t = queue_pull(queue);
   return __builtin_amdgcn_readfirstlane(t);
 }
 

@@ -34,17 +34,12 @@ int prof_read_levels(unsigned long long* out) {
 #endif
 
 // ---- K3a ---------------------------------------------------------------------
-__device__ __forceinline__ int reg_stream(JobDev& job, HStream* streams, int32_t* slot, int pidx, int kind,
-                                          gcu8 p, int64_t n, int w, int64_t count) {
-  const int64_t nruns = n / 2 + 2;  // every run but a truncated last one takes >= 2 bytes
-  // blocks close at kHBlock values, kHBlockRuns runs or kHBlockBytes payload bytes
-  const int64_t nblks = count / kHBlock + nruns / kHBlockRuns + n / (kHBlockBytes / 2) + 3;
-  const int64_t rb = (int64_t)atomicAdd((unsigned long long*)&job.run_used, (unsigned long long)nruns);
-  const int64_t bb = (int64_t)atomicAdd((unsigned long long*)&job.blk_used, (unsigned long long)nblks);
-  if (rb + nruns > job.run_cap || bb + nblks > job.blk_cap) {
-    job.status = kCAPACITY;  // the host grows the run arenas and decodes again
-    return -1;
-  }
+// The stream's run table / block index go to the page's region (k_page_list:
+// every run but a truncated last one takes >= 2 bytes; blocks close at
+// kHBlock values, kHBlockRuns runs or kHBlockBytes payload bytes).
+__device__ __forceinline__ int reg_stream(const JobDev& job, const PageDev& pg, HStream* streams, int32_t* slot,
+                                          int pidx, int kind, gcu8 p, int64_t n, int w, int64_t count) {
+  const int64_t rb = pg.run_off, bb = pg.blk_off;
   const int id = pidx * 3 + (kind > 2 ? 2 : kind);
   HStream& S = streams[id];
   S.p = (const uint8_t*)p;
@@ -543,15 +538,20 @@ struct LevelDecoder {
 #pragma unroll
     for (int g = 0; g < 4; g++) wv[g] = (((b16 >> (4 * g)) & 0xfu) * 0x00204081u) & 0x01010101u;
     const int i0 = 16 * lane;
+#ifdef PQG_NOSTORE_EXPERIMENT
+    constexpr bool kStore = false;
+#else
+    constexpr bool kStore = true;
+#endif
     if (i0 >= pre && i0 + 16 <= end) {
-      stg16(a0 + i0, make_uint4(wv[0], wv[1], wv[2], wv[3]));
+      if (kStore) stg16(a0 + i0, make_uint4(wv[0], wv[1], wv[2], wv[3]));
       if (maxl == 1) nn += __builtin_popcount(b16);
     } else if (i0 + 16 > pre && i0 < end) {
       uint32_t vm = 0;
 #pragma unroll
       for (int k = 0; k < 16; k++) {
         if (i0 + k >= pre && i0 + k < end) {
-          *(PQG_G uint8_t*)(a0 + i0 + k) = (uint8_t)((b16 >> k) & 1);
+          if (kStore) *(PQG_G uint8_t*)(a0 + i0 + k) = (uint8_t)((b16 >> k) & 1);
           vm |= 1u << k;
         }
       }
@@ -838,9 +838,8 @@ __device__ __forceinline__ int level_stream(gcu8 p, int64_t n, int w, uint32_t c
 // (as k_levels_expand) of one data page per wave; the value streams are
 // registered for the walker.
 __global__ void __launch_bounds__(64) k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total,
-                                                    int* queue, uint8_t* scratch, HStream* streams, int* vlists,
-                                                    int* vcount, int list_cap, uint8_t* def_arena,
-                                                    uint8_t* rep_arena) {
+                                                    int* queue, uint8_t* scratch, HStream* streams,
+                                                    uint8_t* def_arena, uint8_t* rep_arena) {
   __shared__ __attribute__((aligned(16))) LevShared sh;
   const int lane = lane_id();
   for (;;) {
@@ -848,7 +847,10 @@ __global__ void __launch_bounds__(64) k_page_levels(JobDev* jobs, PageDev* pages
     if (t >= *total) return;
     const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
     const PageDev pg = pages[pidx];
-    if (lane == 0) pages[pidx].hs_rep = pages[pidx].hs_def = pages[pidx].hs_val = -1;
+    if (lane == 0) {
+      pages[pidx].hs_rep = pages[pidx].hs_def = pages[pidx].hs_val = -1;
+      pages[pidx].vmode = -1;
+    }
     if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3)) continue;
     const JobDev job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
@@ -918,16 +920,15 @@ __global__ void __launch_bounds__(64) k_page_levels(JobDev* jobs, PageDev* pages
       if (pg.encoding == 8 && vn >= 1) {
         const int wv = val[0];
         P.dict_width = wv;
-        if (wv >= 1 && wv <= 32 && n > 0) reg_stream(jobs[pg.job], streams, &P.hs_val, pidx, 2, val + 1, vn - 1, wv, n);
+        if (wv >= 1 && wv <= 32 && n > 0) reg_stream(job, pg, streams, &P.hs_val, pidx, 2, val + 1, vn - 1, wv, n);
       } else if (pg.encoding == 3 && job.type == 0 && vn >= 4) {
         const int64_t sz = rd_u32(val);
         const int64_t take = min(sz, vn - 4);
-        if (n > 0) reg_stream(jobs[pg.job], streams, &P.hs_val, pidx, 3, val + 4, take, 1, n);
+        if (n > 0) reg_stream(job, pg, streams, &P.hs_val, pidx, 3, val + 4, take, 1, n);
       }
       // value-stage page lists: 4-byte dictionary pages (the hot path, a kernel
       // of its own), variable-length values (pqg_strings.hip) and everything else
-      const int mode = job.value_width == 0 ? 2 : (pg.encoding == 8 && job.value_width == 4) ? 1 : 0;
-      vlists[mode * list_cap + atomicAdd(&vcount[mode], 1)] = pidx;
+      P.vmode = job.value_width == 0 ? 2 : (pg.encoding == 8 && job.value_width == 4) ? 1 : 0;
     }
     // ---- readValues (page_v1.go:27-55): rep levels, then def levels
     int64_t nn = 0;

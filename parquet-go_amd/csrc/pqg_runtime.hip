@@ -26,8 +26,9 @@ int pack_levels_launch(hipStream_t s, const uint8_t* levels, int64_t n, int bw, 
 
 namespace pqg {
 __global__ void k_page_cands(JobDev* jobs, int n_jobs, int* tile_count, int* tile_okc, int64_t* cand_pos,
-                             int* cand_list, int* cand_total);
-__global__ void k_cand_parse(JobDev* jobs, int n_jobs, const int* cand_list, const int* cand_total, int* tile_okc,
+                             int* cand_list, int* cand_total, int region);
+__global__ void k_cand_parse(JobDev* jobs, int n_jobs, const int* cand_list, const int* cand_total, int region,
+                             int* tile_okc,
                              const int64_t* cand_pos, Cand* cands);
 __global__ void k_tile_scan(JobDev* jobs, const int* tile_count, const int* tile_okc, int* tile_off, int* tile_okoff);
 __global__ void k_cand_link(JobDev* jobs, int n_jobs, int64_t total_tiles, const int* tile_count,
@@ -36,12 +37,12 @@ __global__ void k_cand_link(JobDev* jobs, int n_jobs, int64_t total_tiles, const
 __global__ void k_page_chain(JobDev* jobs, PageDev* pages, const Cand* cands, const int* succ,
                              const int* idx2slot, const int* ok2slot, int* order);
 __global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs);
-__global__ void k_page_list(JobDev* jobs, int n_jobs, int* list, int list_cap, int* total, int* queues);
+__global__ void k_page_list(JobDev* jobs, PageDev* pages, int n_jobs, int* list, int list_cap, int* total,
+                            int* queues);
 __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                          uint8_t* scratch);
 __global__ void k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
-                              uint8_t* scratch, HStream* streams, int* vlists, int* vcount, int list_cap,
-                              uint8_t* def_arena, uint8_t* rep_arena);
+                              uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena);
 __global__ void k_hybrid_walk(const PageDev* pages, const int* list, const int* total, HStream* streams,
                               RunEnt* runs, BlockDesc* blks);
 __global__ void k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch);
@@ -151,6 +152,7 @@ struct pqg_ctx {
   std::map<JobKey, Caps> learned;       // grown capacities, across calls
   int launches = 0;                     // pipeline launches of the last decode
   bool any_var = false;                 // batch holds variable-length columns
+  bool any_fixed_other = false;         // batch holds fixed-width columns (k_values<0> pages possible)
   int n_jobs = 0;
   int64_t list_cap = 0;
   hipEvent_t ev[kStages + 1];
@@ -339,7 +341,7 @@ static int plan_batch(pqg_ctx* c) {
       c->tile_okoff.grow(sizeof(int) * (size_t)tile_total + 64) ||
       c->ok2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->cand_pos.grow(sizeof(int64_t) * (size_t)tile_total * kCandPerTile + 64) ||
-      c->cand_list.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
+      c->cand_list.grow(sizeof(int) * (size_t)(tile_total + kQShards) * kCandPerTile + 64) ||
       c->vlists.grow(sizeof(int) * 3 * (size_t)page_total + 64) ||
       c->cands.grow(sizeof(Cand) * (size_t)tile_total * kCandPerTile + 64) ||
       c->succ.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
@@ -360,14 +362,19 @@ static int launch_pipeline(pqg_ctx* c) {
   JobDev* jobs = (JobDev*)c->jobs.p;
   PageDev* pages = (PageDev*)c->pages.p;
   int* list = (int*)c->list.p;
-  int* ctr = (int*)c->counters.p;  // [0] total pages, [8..15] queues
+  int* ctr = (int*)c->counters.p;  // [0] total pages in the list
+  // work queues (sharded over the XCDs, see queue_pull): 0 snappy, 1 levels,
+  // 2 values<0>, 3 values<1>, 4 str_count, 5 str_plain, 6 str_copy, 7 the
+  // candidate list heads of k_page_cands
+  auto Q = [&](int k) { return ctr + 1024 + k * kQueueInts; };
   uint8_t* scratch = (uint8_t*)c->scratch.p;
   // page-queue kernels: one wave per page; enough waves per SIMD to hide the
-  // dependent HBM reads of the run walks (bounded by VGPRs / LDS per kernel)
+  // dependent HBM reads (bounded by VGPRs / LDS per kernel)
   const int waves = c->num_cus * 20;
   const int snappy_waves = c->num_cus * 2;  // 68 KiB LDS each (64 KiB output history)
   hipStream_t s = c->stream;
   if (c->timed) hipEventRecord(c->ev[0], s);
+  hipMemsetAsync(Q(0), 0, sizeof(int) * 8 * kQueueInts, s);
   const int64_t nt = c->total_tiles;
   int* tcount = (int*)c->tile_count.p;
   int* toff = (int*)c->tile_off.p;
@@ -377,11 +384,11 @@ static int launch_pipeline(pqg_ctx* c) {
   if (nt > 0) {
     int64_t* cpos = (int64_t*)c->cand_pos.p;
     int* clist = (int*)c->cand_list.p;
-    int* ctotal = ctr + 16;  // zeroed below, counted by k_page_cands
-    hipMemsetAsync(ctotal, 0, sizeof(int), s);
-    hipLaunchKernelGGL(k_page_cands, dim3((unsigned)nt), dim3(256), 0, s, jobs, n, tcount, tokc, cpos, clist, ctotal);
+    const int region = (int)((nt + kQShards - 1) / kQShards) * kCandPerTile;  // one list region per head
+    hipLaunchKernelGGL(k_page_cands, dim3((unsigned)nt), dim3(256), 0, s, jobs, n, tcount, tokc, cpos, clist, Q(7),
+                       region);
     hipLaunchKernelGGL(k_cand_parse, dim3((unsigned)std::min<int64_t>((nt * kCandPerTile + 255) / 256, c->num_cus * 4)),
-                       dim3(256), 0, s, jobs, n, clist, ctotal, tokc, cpos, cands);
+                       dim3(256), 0, s, jobs, n, clist, Q(7), region, tokc, cpos, cands);
   }
   hipLaunchKernelGGL(k_tile_scan, dim3(n), dim3(1024), 0, s, jobs, tcount, tokc, toff, tokoff);
   if (nt > 0)
@@ -391,23 +398,21 @@ static int launch_pipeline(pqg_ctx* c) {
                      (const int*)c->idx2slot.p, (const int*)c->ok2slot.p, (int*)c->order.p);
   hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n);
   if (c->timed) hipEventRecord(c->ev[1], s);
-  hipLaunchKernelGGL(k_page_list, dim3(1), dim3(256), 0, s, jobs, n, list, (int)std::min<int64_t>(c->list_cap, INT32_MAX),
-                     ctr, ctr + 8);
+  hipLaunchKernelGGL(k_page_list, dim3(n), dim3(256), 0, s, jobs, pages, n, list,
+                     (int)std::min<int64_t>(c->list_cap, INT32_MAX), ctr, ctr + 8);
   if (c->timed) hipEventRecord(c->ev[2], s);
   bool any_comp = false;
   for (int i = 0; i < n; i++) any_comp |= c->cur[(size_t)i].col.codec != PQG_CODEC_UNCOMPRESSED;
   if (any_comp) {
-    hipLaunchKernelGGL(k_snappy, dim3(snappy_waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 8, scratch);
+    hipLaunchKernelGGL(k_snappy, dim3(snappy_waves), dim3(64), 0, s, jobs, pages, list, ctr, Q(0), scratch);
   }
   if (c->timed) hipEventRecord(c->ev[3], s);
   HStream* streams = (HStream*)c->streams.p;
   RunEnt* runs = (RunEnt*)c->runs.p;
   BlockDesc* blks = (BlockDesc*)c->blks.p;
-  int* vlists = (int*)c->vlists.p;
-  const int lcap = (int)std::min<int64_t>(c->list_cap, INT32_MAX);
   // setup + def/rep levels, one wave per data page (value streams registered for the walk)
-  hipLaunchKernelGGL(k_page_levels, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, ctr + 9, scratch, streams,
-                     vlists, ctr + 12, lcap, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p);
+  hipLaunchKernelGGL(k_page_levels, dim3(c->num_cus * 24), dim3(64), 0, s, jobs, pages, list, ctr, Q(1), scratch,
+                     streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p);
   if (c->timed) hipEventRecord(c->ev[4], s);
   const unsigned walk_blocks =
       (unsigned)std::max<int64_t>(1, std::min<int64_t>((c->list_cap + 255) / 256, c->num_cus * 8));
@@ -416,21 +421,23 @@ static int launch_pipeline(pqg_ctx* c) {
   if (c->timed) hipEventRecord(c->ev[6], s);
   hipLaunchKernelGGL(k_nn_scan, dim3(n), dim3(256), 0, s, jobs, pages, scratch);
   if (c->timed) hipEventRecord(c->ev[7], s);
-  hipLaunchKernelGGL(k_values<1>, dim3(waves), dim3(64), 0, s, jobs, pages, vlists + lcap, ctr + 13, ctr + 11,
+  // every values kernel takes the whole page list and keeps the pages whose
+  // vmode (set by k_page_levels) is its own
+  hipLaunchKernelGGL(k_values<1>, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, Q(3),
                      (uint8_t*)c->value_arena.p, streams, runs, blks);
-  hipLaunchKernelGGL(k_values<0>, dim3(waves), dim3(64), 0, s, jobs, pages, vlists, ctr + 12, ctr + 10,
-                     (uint8_t*)c->value_arena.p, streams, runs, blks);
+  if (c->any_fixed_other)
+    hipLaunchKernelGGL(k_values<0>, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, Q(2),
+                       (uint8_t*)c->value_arena.p, streams, runs, blks);
   if (c->timed) hipEventRecord(c->ev[8], s);
   if (c->any_var) {
     int64_t* offs = (int64_t*)c->offs_arena.p;
     hipLaunchKernelGGL(k_str_dict, dim3(n), dim3(512), 0, s, jobs, pages, (int64_t*)c->doffs_arena.p);
-    hipLaunchKernelGGL(k_str_plain, dim3(c->num_cus * 4), dim3(512), 0, s, jobs, pages, vlists + 2 * lcap, ctr + 14,
-                       ctr + 19, offs);
-    hipLaunchKernelGGL(k_str_count, dim3(waves), dim3(64), 0, s, jobs, pages, vlists + 2 * lcap, ctr + 14, ctr + 17,
-                       offs, streams, runs, blks);
+    hipLaunchKernelGGL(k_str_plain, dim3(c->num_cus * 4), dim3(512), 0, s, jobs, pages, list, ctr, Q(5), offs);
+    hipLaunchKernelGGL(k_str_count, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, Q(4), offs, streams, runs,
+                       blks);
     hipLaunchKernelGGL(k_char_scan, dim3(n), dim3(256), 0, s, jobs, pages, offs);
-    hipLaunchKernelGGL(k_str_copy, dim3(c->num_cus * 4), dim3(512), 0, s, jobs, pages, vlists + 2 * lcap, ctr + 14,
-                       ctr + 20, (uint8_t*)c->value_arena.p, offs);
+    hipLaunchKernelGGL(k_str_copy, dim3(c->num_cus * 4), dim3(512), 0, s, jobs, pages, list, ctr, Q(6),
+                       (uint8_t*)c->value_arena.p, offs);
   }
   if (c->timed) hipEventRecord(c->ev[9], s);
   hipLaunchKernelGGL(k_finalize, dim3(n), dim3(256), 0, s, jobs, n, pages);
@@ -453,10 +460,13 @@ int pqg_decode_chunks_async(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs) {
   c->launches = 0;
   c->force.assign((size_t)n_jobs, Caps());
   c->any_var = false;
+  c->any_fixed_other = false;
   for (int i = 0; i < n_jobs; i++) {
     auto it = c->learned.find(JobKey{(uintptr_t)jobs[i].data, jobs[i].total_compressed_size, jobs[i].num_values_hint});
     if (it != c->learned.end()) c->force[(size_t)i] = it->second;
     c->any_var |= value_width_of(jobs[i].col) == 0;
+    // k_values<0>: every fixed-width column but 4-byte ones with only dictionary pages
+    c->any_fixed_other |= value_width_of(jobs[i].col) != 0;
   }
   if (n_jobs == 0) return PQG_OK;
   int e = plan_batch(c);

@@ -130,7 +130,8 @@ __device__ __forceinline__ void init_page(PageDev& pg, int j, int64_t pos, int64
   pg.not_null = 0;
   pg.flags = 0;
   pg.dict_width = 0;
-  pg.pad = 0;
+  pg.vmode = -1;
+  pg.run_off = pg.blk_off = 0;
   pg.chars = 0;
   pg.char_offset = 0;
 }
@@ -249,8 +250,11 @@ __device__ __forceinline__ void parse_candidate(const JobDev& job, int64_t p, Sk
   *out = cd;
 }
 
+// cand_total: kQShards counters kQStride ints apart; tile t appends to shard
+// t & 7, whose list region starts at (t & 7) * region (a single list head
+// would take one contended device-scope atomic per tile).
 __global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, int n_jobs, int* tile_count, int* tile_okc,
-                                                    int64_t* cand_pos, int* cand_list, int* cand_total) {
+                                                    int64_t* cand_pos, int* cand_list, int* cand_total, int region) {
   __shared__ int cnt;
   __shared__ int job_s;
   __shared__ int64_t loc[kCandPerTile];
@@ -313,7 +317,10 @@ __global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, int n_jobs, in
     tile_okc[tile] = 0;  // counted by k_cand_parse
   }
   __shared__ int list_base;
-  if (tid == 0 && n > 0 && n <= kCandPerTile) list_base = atomicAdd(cand_total, n);
+  if (tid == 0 && n > 0 && n <= kCandPerTile) {
+    const int sh = (int)(tile & (kQShards - 1));
+    list_base = sh * region + atomicAdd(cand_total + sh * kQStride, n);
+  }
   __syncthreads();
   if (n <= kCandPerTile && tid < n) {  // rank sort by position (positions are distinct)
     const int64_t me = loc[tid];
@@ -328,13 +335,20 @@ __global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, int n_jobs, in
 // One lane per candidate slot: parse + classify (kept apart from the byte scan
 // so that the scan has no scratch and runs at full occupancy).
 __global__ void __launch_bounds__(256) k_cand_parse(JobDev* jobs, int n_jobs, const int* cand_list,
-                                                    const int* cand_total, int* tile_okc, const int64_t* cand_pos,
-                                                    Cand* cands) {
+                                                    const int* cand_total, int region, int* tile_okc,
+                                                    const int64_t* cand_pos, Cand* cands) {
   __shared__ SkipFrame frames[256][kCandFrames];
   __shared__ int16_t lasts[256][kCandLast];
-  const int nc = *cand_total;
+  int pre[kQShards + 1];  // the shards' list lengths, prefix-summed (uniform)
+  pre[0] = 0;
+#pragma unroll
+  for (int k = 0; k < kQShards; k++) pre[k + 1] = pre[k] + cand_total[k * kQStride];
+  const int nc = pre[kQShards];
   for (int i = blockIdx.x * 256 + threadIdx.x; i < nc; i += gridDim.x * 256) {
-    const int slot = cand_list[i];
+    int sh = 0;
+#pragma unroll
+    for (int k = 1; k < kQShards; k++) sh += i >= pre[k];
+    const int slot = cand_list[sh * region + (i - pre[sh])];
     const int64_t tile = slot / kCandPerTile;
     int lo = 0, hi = n_jobs - 1;
     while (lo < hi) {
@@ -694,19 +708,64 @@ __global__ void __launch_bounds__(64) k_scan_pages(JobDev* jobs, PageDev* pages,
 // ============================================================================
 // K1f: compact list of page indices over all jobs.
 // ============================================================================
-__global__ void k_page_list(JobDev* jobs, int n_jobs, int* list, int list_cap, int* total, int* queues) {
-  int off = 0;
-  for (int j = 0; j < n_jobs; j++) {
-    int n = jobs[j].num_pages;
-    if (n > jobs[j].page_cap) n = jobs[j].page_cap;
-    if (jobs[j].status == kCAPACITY) n = 0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x)
-      if (off + i < list_cap) list[off + i] = (int)(jobs[j].page_base + i);
-    off += n;
+// One 256-lane block per job: the job's pages in the list (at the offset of
+// the pages of the jobs before it), and each data page's region of the value
+// stream's run table / block index — an exclusive scan of a bound from the
+// page's sizes (the same bound reg_stream used to take with two contended
+// atomics per page): a value stream of B bytes and n values has at most
+// B/2 + 2 runs and n/kHBlock + runs/kHBlockRuns + B/(kHBlockBytes/2) + 3 blocks.
+__global__ void __launch_bounds__(256) k_page_list(JobDev* jobs, PageDev* pages, int n_jobs, int* list, int list_cap,
+                                                   int* total, int* queues) {
+  __shared__ int64_t part[5];
+  __shared__ int s_off;
+  const int j = blockIdx.x;
+  auto pages_of = [&](int i) {
+    int n = jobs[i].num_pages;
+    if (n > jobs[i].page_cap) n = jobs[i].page_cap;
+    if (jobs[i].status == kCAPACITY) n = 0;
+    return n;
+  };
+  if (threadIdx.x == 0) {
+    int off = 0;
+    for (int i = 0; i < j; i++) off += pages_of(i);
+    s_off = off;
+    if (j == n_jobs - 1) {
+      const int all = off + pages_of(j);
+      *total = all < list_cap ? all : list_cap;
+      for (int q = 0; q < 16; q++) queues[q] = 0;  // ctr[8..23]
+    }
+  }
+  __syncthreads();
+  const int off = s_off;
+  JobDev& job = jobs[j];
+  const int n = pages_of(j);
+  int64_t rc = 0, bc = 0;
+  for (int b = 0; b < n; b += 256) {
+    const int i = b + threadIdx.x;
+    int64_t nr = 0, nb = 0;
+    if (i < n) {
+      if (off + i < list_cap) list[off + i] = (int)(job.page_base + i);
+      PageDev& pg = pages[job.page_base + i];
+      if (pg.page_type == 0 || pg.page_type == 3) {
+        const int64_t B = pg.scratch_offset >= 0 ? (int64_t)(uint32_t)pg.usize : (int64_t)(uint32_t)pg.csize;
+        nr = B / 2 + 2;
+        nb = (int64_t)(uint32_t)pg.num_values / kHBlock + nr / kHBlockRuns + B / (kHBlockBytes / 2) + 3;
+      }
+    }
+    int64_t tr, tb;
+    const int64_t er = block_excl_scan<256>(nr, &tr, part);
+    const int64_t eb = block_excl_scan<256>(nb, &tb, part);
+    if (i < n) {
+      pages[job.page_base + i].run_off = rc + er;
+      pages[job.page_base + i].blk_off = bc + eb;
+    }
+    rc += tr;
+    bc += tb;
   }
   if (threadIdx.x == 0) {
-    *total = off < list_cap ? off : list_cap;
-    for (int q = 0; q < 16; q++) queues[q] = 0;  // ctr[8..23]: queues and list counts
+    job.run_used = rc;
+    job.blk_used = bc;
+    if (rc > job.run_cap || bc > job.blk_cap) job.status = kCAPACITY;  // the host grows the run arenas
   }
 }
 

@@ -314,14 +314,14 @@ __global__ void __launch_bounds__(kWalkT) k_str_plain(JobDev* jobs, PageDev* pag
   __shared__ BlockWalkShared sh;
   __shared__ int s_t;
   for (;;) {
-    if (threadIdx.x == 0) s_t = atomicAdd(queue, 1);
+    if (threadIdx.x == 0) s_t = queue_pull(queue);
     __syncthreads();
     const int t = s_t;
     __syncthreads();
     if (t >= *total) return;
     const int pidx = list[t];
     const PageDev& pg = pages[pidx];
-    if (pg.read_status != kOK || pg.decode_status != kOK || (pg.page_type != 0 && pg.page_type != 3) ||
+    if (pg.read_status != kOK || pg.decode_status != kOK || (pg.page_type != 0 && pg.page_type != 3) || pg.vmode != 2 ||
         pg.encoding != 0 || pg.not_null == 0)
       continue;
     const JobDev& job = jobs[pg.job];
@@ -391,7 +391,7 @@ __global__ void __launch_bounds__(64) k_str_count(JobDev* jobs, PageDev* pages, 
     if (t >= *total) return;
     const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
     const PageDev pg = pages[pidx];
-    if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3)) continue;
+    if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3) || pg.vmode != 2) continue;
     const JobDev job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
     const int enc = pg.encoding;
@@ -490,7 +490,7 @@ __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, 
   __shared__ int64_t part[9];
   for (;;) {
     if (threadIdx.x == 0) {
-      s_t = atomicAdd(queue, 1);
+      s_t = queue_pull(queue);
       s_prev = 0;
     }
     __syncthreads();
@@ -499,7 +499,7 @@ __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, 
     if (t >= *total) return;
     const int pidx = list[t];
     const PageDev& pg = pages[pidx];
-    if (pg.read_status != kOK || pg.decode_status != kOK || (pg.page_type != 0 && pg.page_type != 3) ||
+    if (pg.read_status != kOK || pg.decode_status != kOK || (pg.page_type != 0 && pg.page_type != 3) || pg.vmode != 2 ||
         pg.not_null == 0)
       continue;
     const JobDev& job = jobs[pg.job];

@@ -358,7 +358,9 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
     // locals (see k_levels_expand); results are written back at the end
     const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
     const PageDev pg = pages[pidx];
-    if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3)) continue;
+    // every data page of the list is set up by k_page_levels, which also
+    // chose its values stage (vmode)
+    if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3) || pg.vmode != Mode) continue;
     const JobDev job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
     const gcu8 val = gconst(pg.val);
