@@ -116,6 +116,25 @@ __device__ __forceinline__ void block_values(const ExpandShared& sh, int b, cons
   }
 }
 
+// Block b holds a single run (nr == 1, the common case: runs of <= 512
+// values start the blocks): no run marks or scans, the run's fields come in
+// scalars (st = its start | kRunBP, src).
+__device__ __forceinline__ void block_values_1(const ExpandShared& sh, int b, const BlockGeom& g, uint32_t st,
+                                               uint32_t src, uint32_t mask, int w, int lane, uint32_t (&v)[8]) {
+  if (!(st & kRunBP)) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) v[q] = src;
+    return;
+  }
+  const uint32_t rb0 = (uint32_t)((int64_t)src * 8 - g.sb * 8) + (g.v0 + lane * 8 - (st & ~kRunBP)) * (uint32_t)w;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint32_t rb = rb0 + (uint32_t)(q * w);
+    const uint32_t d = rb >> 5;
+    v[q] = __builtin_amdgcn_alignbit(sh.stage[b][d + 1], sh.stage[b][d], rb & 31) & mask;
+  }
+}
+
 // Sink:
 //   void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup], const int (&cnt)[kGroup])
 // values v[b][0..cnt[b]) belong at value indices i0[b]...; cnt[b] == 0: none.
@@ -178,7 +197,7 @@ __device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int b = 0; b < kGroup; b++) {
-        *(PQG_L u32x2_t*)(lds_ptr(sh.rmap[b]) + 8 * lane) = u32x2_t{0u, 0u};
+        if (g[b].nr > 1) *(PQG_L u32x2_t*)(lds_ptr(sh.rmap[b]) + 8 * lane) = u32x2_t{0u, 0u};
         if ((uint32_t)lane < g[b].nr) {
           sh.runs[b][lane].start = rs[b];
           sh.runs[b][lane].src = rv[b];
@@ -200,7 +219,11 @@ __device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __
       for (int b = 0; b < kGroup; b++) {
         i0[b] = g[b].v0 + lane * 8;
         cnt[b] = (k0 + b < nk && i0[b] < g[b].v1) ? (int)(g[b].v1 - i0[b] < 8 ? g[b].v1 - i0[b] : 8) : 0;
-        block_values(sh, b, g[b], mask, w, lane, v[b]);
+        if (g[b].nr == 1)
+          block_values_1(sh, b, g[b], (uint32_t)__builtin_amdgcn_readfirstlane(rs[b]),
+                         (uint32_t)__builtin_amdgcn_readfirstlane(rv[b]), mask, w, lane, v[b]);
+        else
+          block_values(sh, b, g[b], mask, w, lane, v[b]);
       }
       PQG_T(t3);
       PQG_ACC(2, t2, t3);

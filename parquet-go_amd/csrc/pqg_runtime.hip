@@ -135,6 +135,7 @@ struct pqg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int num_cus = 256;
+  int snappy_per_cu = 2;  // resident k_snappy waves per CU (LDS-bound: the output history ring)
   DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
   DevBuf tile_count, tile_okc, tile_off, tile_okoff, cand_pos, cands, succ, idx2slot, ok2slot, order;  // K1
   DevBuf streams, runs, blks;  // K3 hybrid run tables
@@ -202,6 +203,11 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
     return PQG_ERR_HIP;
   }
   for (auto& e : c->ev) hipEventCreate(&e);
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&k_snappy), 64, 0) ==
+          hipSuccess &&
+      occ > 0)
+    c->snappy_per_cu = occ;
   c->counters.grow(4096);
   *out = c;
   return PQG_OK;
@@ -371,7 +377,7 @@ static int launch_pipeline(pqg_ctx* c) {
   // page-queue kernels: one wave per page; enough waves per SIMD to hide the
   // dependent HBM reads (bounded by VGPRs / LDS per kernel)
   const int waves = c->num_cus * 20;
-  const int snappy_waves = c->num_cus * 2;  // 68 KiB LDS each (64 KiB output history)
+  const int snappy_waves = c->num_cus * c->snappy_per_cu;  // as many as fit (LDS: the history ring)
   hipStream_t s = c->stream;
   if (c->timed) hipEventRecord(c->ev[0], s);
   hipMemsetAsync(Q(0), 0, sizeof(int) * 8 * kQueueInts, s);

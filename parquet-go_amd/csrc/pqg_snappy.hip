@@ -54,8 +54,14 @@ constexpr int kDense = 4;         // tags in a window for the batched byte resol
 constexpr int kSnWin = 4096;      // compressed-stream window (LDS)
 constexpr int kSnWinNeed = 2048;  // window bytes wanted ahead of the first tag
 constexpr int kSpan = 1024;       // output bytes a batch covers: 64 lanes x one 16-byte granule
-constexpr int kRing = 65536;      // output history kept in LDS
-constexpr int kSnFlush = 16384;   // flush granularity (a wave's stores are waited for at the next loop head)
+#ifndef PQG_SNAPPY_RING
+#define PQG_SNAPPY_RING 16384
+#endif
+constexpr int kRing = PQG_SNAPPY_RING;  // output history kept in LDS (a power of two)
+// flush granularity (a wave's stores are waited for at the next loop head);
+// unflushed bytes (< kSnFlush + a batch or literal piece) must stay inside the ring
+constexpr int kSnFlush = kRing / 4 < 16384 ? kRing / 4 : 16384;
+static_assert((kRing & (kRing - 1)) == 0 && kRing >= 8192, "ring: a power of two >= 8 KiB");
 constexpr int kLongPiece = 4096;  // literal piece read from HBM
 constexpr int kWinLit = 1024;     // literals up to this many bytes (after the granule prefix) move from the window
 
@@ -154,6 +160,14 @@ struct SnapBlock {
   int64_t d = 0;        // output bytes produced
   int64_t flushed = 0;  // output bytes stored (16-aligned until the end)
   int64_t in_base = kFarAway;
+#ifdef PQG_PROFILE
+  uint64_t pacc[16] = {0};
+#define PQG_ST(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define PQG_SA(k, x) pacc[k] += (x)
+#else
+#define PQG_ST(v)
+#define PQG_SA(k, x)
+#endif
 
   // window [in_base, in_base + kSnWin) over the compressed block, 16-aligned in memory
   __device__ void fill(int64_t at) {
@@ -368,6 +382,7 @@ struct SnapBlock {
       } else {
         copy_bytes(offset, (int)length);
       }
+      maybe_flush();  // keeps the unflushed tail inside the ring
       s = ns;
       if (!next_in) break;
       x8 = nx8;
@@ -382,16 +397,24 @@ struct SnapBlock {
   // above d.
   __device__ int run(int64_t s) {
     const int lane = lane_id();
+    PQG_ST(t_run0);
     const PQG_L uint8_t* IN = lds_ptr(sh->in);
     int serial_next = 0;  // tags to take one at a time before the next windowed resolution
     while (s < slen) {
+      PQG_ST(ta);
+      PQG_SA(8, 1);
       if (s < in_base || s + kSnWinNeed > in_base + kSnWin) {
         // pending output goes out with the window loads: one wait covers both
         if ((d & ~(int64_t)15) - flushed >= 2048) flush(d & ~(int64_t)15);
         fill(s);
       }
+      PQG_ST(tb);
+      PQG_SA(0, tb - ta);
       if (serial_next > 0) {
+        PQG_SA(11, 1);
         const int e = serial(s, serial_next);
+        PQG_ST(tsx);
+        PQG_SA(7, tsx - tb);
         if (e) return e;
         serial_next = 0;
         continue;
@@ -419,6 +442,8 @@ struct SnapBlock {
         }
       }
       const bool on0 = (cm0 >> lane) & 1, on1 = (cm1 >> lane) & 1;
+      PQG_ST(tc);
+      PQG_SA(1, tc - tb);
       // ---- 3. output offsets and the reference's checks
       const uint32_t o0 = on0 ? (uint32_t)(t0.len < (1 << 30) ? t0.len : (1 << 30)) : 0u;
       const uint32_t o1 = on1 ? (uint32_t)(t1.len < (1 << 30) ? t1.len : (1 << 30)) : 0u;
@@ -463,7 +488,10 @@ struct SnapBlock {
         s1 = s + readlane64(last < 64 ? t0.next : t1.next, last & 63);
       }
       const int64_t d1 = d + out;
+      PQG_ST(td);
+      PQG_SA(2, td - tc);
       if (__popcll(bm0) + __popcll(bm1) < kDense) {
+        PQG_SA(10, 1);
         // ---- 4b. sparse: tag by tag, with the fields already parsed
         uint64_t m0 = bm0, m1 = bm1;
         while (m0 | m1) {
@@ -480,12 +508,17 @@ struct SnapBlock {
           } else {
             copy_bytes((uint32_t)__builtin_amdgcn_readlane((int)(hi ? t1.info : t0.info), l), (int)len);
           }
+          maybe_flush();
         }
         s = s1;
         if ((d & ~(int64_t)15) - flushed >= kSnFlush) flush(d & ~(int64_t)15);
         serial_next = 64;  // a tag-sparse stretch: continue tag by tag
+        PQG_ST(tsp);
+        PQG_SA(3, tsp - td);
         continue;
       }
+      PQG_SA(9, 1);
+      PQG_SA(12, __popcll(bm0) + __popcll(bm1));
       // ---- 4a. dense: per-byte sources for the granules from a0
       const int end = pre + (int)out;  // batch bytes [pre, end)
       PQG_L uint8_t* TM = lds_ptr(sh->tmap);
@@ -528,6 +561,8 @@ struct SnapBlock {
         // history bytes before d stay as they are; bytes past the batch read any terminal
         own[k] = idx < pre ? idx : idx >= end ? kSpan : v;
       }
+      PQG_ST(te);
+      PQG_SA(4, te - td);
       // same-batch copy sources: pointer doubling over src[]
       bool chase = false;
 #pragma unroll
@@ -551,9 +586,12 @@ struct SnapBlock {
             chase |= own[k] >= pre && own[k] < kSpan;
           }
           __builtin_amdgcn_wave_barrier();
+          PQG_SA(13, 1);
           if (!__ballot(chase)) break;
         }
       }
+      PQG_ST(tf);
+      PQG_SA(5, tf - te);
       // every byte reads its source once: the window or the ring (one LDS
       // byte load at a computed address), or, older than the ring, L2
       const int64_t ring_lo = ((d + 15) & ~(int64_t)15) - kRing;
@@ -570,6 +608,7 @@ struct SnapBlock {
         bt[k] = shb[off];
       }
       if (__ballot(far)) {
+        PQG_SA(14, 1);
         // flushed output, read through L2: wait for the flush stores, then
         // invalidate this CU's L1 (a line loaded earlier may hold bytes that
         // were stored after it was cached)
@@ -599,7 +638,11 @@ struct SnapBlock {
       d = d1;
       s = s1;
       maybe_flush();
+      PQG_ST(tg);
+      PQG_SA(6, tg - tf);
     }
+    PQG_ST(t_run1);
+    PQG_SA(15, t_run1 - t_run0);
     if (d != dlen) return kSNAPPY;
     flush((dlen + 15) & ~(int64_t)15);
     return kOK;
@@ -650,6 +693,9 @@ __global__ void __launch_bounds__(64) k_snappy(JobDev* jobs, PageDev* pages, con
     if (e == kOK && v > 0xffffffffull) e = kSNAPPY;
     if (e == kOK && (int64_t)v != ulen) e = kSIZE;
     if (e == kOK) e = blk.run(hl);
+#ifdef PQG_PROFILE
+    for (int k = 0; k < 16; k++) PQG_ACC(k, 0, blk.pacc[k]);
+#endif
     // V1: getValuesDecoder runs after the block is decompressed (page_v1.go:91-97)
     if (e == kOK && pg.page_type == 0 && !values_supported(job.type, job.type_length, pg.encoding)) e = kUNSUPPORTED;
     if (lane == 0 && e != kOK) pages[pidx].read_status = e;

@@ -43,6 +43,38 @@ struct DictSink {
   int w;
   __device__ __forceinline__ void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup],
                                         const int (&cnt)[kGroup]) {
+    if (W == 4) {
+      // common case: every key of the group is valid (one max + one ballot
+      // instead of a check per value)
+      uint32_t mx = 0;
+#pragma unroll
+      for (int b = 0; b < kGroup; b++)
+#pragma unroll
+        for (int q = 0; q < 8; q++) mx = q < cnt[b] && v[b][q] > mx ? v[b][q] : mx;
+      if (!__ballot((int64_t)mx >= count)) {
+        uint32_t gv[kGroup][8];
+        const PQG_G uint32_t* d = (const PQG_G uint32_t*)dict;
+#pragma unroll
+        for (int b = 0; b < kGroup; b++)
+#pragma unroll
+          for (int q = 0; q < 8; q++) gv[b][q] = d[q < cnt[b] ? v[b][q] : 0u];
+#pragma unroll
+        for (int b = 0; b < kGroup; b++) {
+          if (cnt[b] == 0) continue;
+          const uintptr_t o = (uintptr_t)(out + (int64_t)i0[b] * 4);
+          if (cnt[b] == 8 && (o & 15) == 0) {
+            stg16(o, make_uint4(gv[b][0], gv[b][1], gv[b][2], gv[b][3]));
+            stg16(o + 16, make_uint4(gv[b][4], gv[b][5], gv[b][6], gv[b][7]));
+          } else if (cnt[b] == 8 && (o & 7) == 0) {
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) stg8(o + 4 * q, gv[b][q], gv[b][q + 1]);
+          } else {
+            for (int q = 0; q < cnt[b]; q++) ((PQG_G uint32_t*)o)[q] = gv[b][q];
+          }
+        }
+        return;
+      }
+    }
     bool ok[kGroup][8];
 #pragma unroll
     for (int b = 0; b < kGroup; b++)
