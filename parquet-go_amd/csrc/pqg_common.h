@@ -69,7 +69,7 @@ struct PageDev {
   int32_t flags;
   int32_t dict_width;      // RLE_DICTIONARY: index bit width byte
   int32_t hs_rep, hs_def, hs_val;  // hybrid streams of the page (HStream index, -1: none)
-  int32_t vmode;           // values stage of the page: 1 4-byte dictionary, 0 other fixed width, 2 variable, -1 none
+  int32_t vmode;           // values stage of the page: 1 4-byte dictionary, 3 DELTA_BINARY_PACKED, 0 other fixed width, 2 variable, -1 none
   int64_t run_off, blk_off;  // the page's run-table / block-index region (job-relative, k_page_list)
   // variable-length values (BYTE_ARRAY, FLBA of length 0): chars of the page
   // and their offset in the chunk's chars (exclusive scan over the pages)
@@ -162,6 +162,10 @@ struct JobDev {
 constexpr int kQShards = 8;
 constexpr int kQStride = 32;
 constexpr int kQueueInts = kQShards * kQStride;
+// ints after the counters base (ctr[0] = page-list total): one flag per values
+// stage (PageDev.vmode 0..3), set by k_page_levels when a page of that stage
+// exists, so an empty stage's kernel exits at once instead of walking the list
+constexpr int kModePresentOff = 1024 + 9 * kQueueInts;
 
 // Scan tiles of the speculative page-header search.
 constexpr int kScanTile = 16384;

@@ -587,13 +587,17 @@ struct LevelDecoder {
       };
       const int n0 = nxt(r0, lane), n1 = nxt(r1, 64 + lane);
       // ---- 2. the chain
+      // (two tight loops, one per half: a bit set, a readlane and a compare
+      // per run, so the CU's shared scalar unit is not the bottleneck)
       uint64_t cm0 = 0, cm1 = 0;
       int pp = 0;
+      while (pp < 64) {
+        cm0 |= 1ull << pp;
+        pp = __builtin_amdgcn_readlane(n0, pp);
+      }
       while (pp < kLPos) {
-        const int l = pp & 63;
-        const int a = __builtin_amdgcn_readlane(n0, l), b = __builtin_amdgcn_readlane(n1, l);
-        if (pp < 64) { cm0 |= 1ull << l; pp = a; }
-        else { cm1 |= 1ull << l; pp = b; }
+        cm1 |= 1ull << (pp - 64);
+        pp = __builtin_amdgcn_readlane(n1, pp - 64);
       }
       const bool on0 = (cm0 >> lane) & 1, on1 = (cm1 >> lane) & 1;
       PQG_LT(tc);
@@ -928,7 +932,13 @@ __global__ void __launch_bounds__(64) k_page_levels(JobDev* jobs, PageDev* pages
       }
       // value-stage page lists: 4-byte dictionary pages (the hot path, a kernel
       // of its own), variable-length values (pqg_strings.hip) and everything else
-      P.vmode = job.value_width == 0 ? 2 : (pg.encoding == 8 && job.value_width == 4) ? 1 : 0;
+      const int vm = job.value_width == 0                            ? 2
+                     : (pg.encoding == 8 && job.value_width == 4) ? 1
+                     : pg.encoding == 5                           ? 3
+                                                                  : 0;
+      P.vmode = vm;
+      int* present = const_cast<int*>(total) + kModePresentOff;
+      if (present[vm] == 0) present[vm] = 1;
     }
     // ---- readValues (page_v1.go:27-55): rep levels, then def levels
     int64_t nn = 0;

@@ -371,7 +371,8 @@ static int launch_pipeline(pqg_ctx* c) {
   int* ctr = (int*)c->counters.p;  // [0] total pages in the list
   // work queues (sharded over the XCDs, see queue_pull): 0 snappy, 1 levels,
   // 2 values<0>, 3 values<1>, 4 str_count, 5 str_plain, 6 str_copy, 7 the
-  // candidate list heads of k_page_cands
+  // candidate list heads of k_page_cands, 8 values<3> (DELTA_BINARY_PACKED); then
+  // the per-stage page flags (kModePresentOff)
   auto Q = [&](int k) { return ctr + 1024 + k * kQueueInts; };
   uint8_t* scratch = (uint8_t*)c->scratch.p;
   // page-queue kernels: one wave per page; enough waves per SIMD to hide the
@@ -380,7 +381,7 @@ static int launch_pipeline(pqg_ctx* c) {
   const int snappy_waves = c->num_cus * c->snappy_per_cu;  // as many as fit (LDS: the history ring)
   hipStream_t s = c->stream;
   if (c->timed) hipEventRecord(c->ev[0], s);
-  hipMemsetAsync(Q(0), 0, sizeof(int) * 8 * kQueueInts, s);
+  hipMemsetAsync(Q(0), 0, sizeof(int) * 10 * kQueueInts, s);  // queues + the stage flags (kModePresentOff)
   const int64_t nt = c->total_tiles;
   int* tcount = (int*)c->tile_count.p;
   int* toff = (int*)c->tile_off.p;
@@ -431,9 +432,12 @@ static int launch_pipeline(pqg_ctx* c) {
   // vmode (set by k_page_levels) is its own
   hipLaunchKernelGGL(k_values<1>, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, Q(3),
                      (uint8_t*)c->value_arena.p, streams, runs, blks);
-  if (c->any_fixed_other)
+  if (c->any_fixed_other) {
     hipLaunchKernelGGL(k_values<0>, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, Q(2),
                        (uint8_t*)c->value_arena.p, streams, runs, blks);
+    hipLaunchKernelGGL(k_values<3>, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, Q(8),
+                       (uint8_t*)c->value_arena.p, streams, runs, blks);
+  }
   if (c->timed) hipEventRecord(c->ev[8], s);
   if (c->any_var) {
     int64_t* offs = (int64_t*)c->offs_arena.p;

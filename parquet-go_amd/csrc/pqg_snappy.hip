@@ -428,18 +428,19 @@ struct SnapBlock {
       // ---- 2. the chain, one v_readlane per tag
       uint64_t cm0 = 0, cm1 = 0;
       int p = 0, last = 0;
-      const int64_t lim = slen - s;  // tags start before the end of the block
-      while (p < kPos && p < lim) {
+      const int64_t lim64 = slen - s;  // tags start before the end of the block
+      const int lim = lim64 < kPos ? (int)lim64 : kPos;
+      // one tight loop per half (a bit set, a readlane, a compare per tag)
+      const int lim0 = lim < 64 ? lim : 64;
+      while (p < lim0) {
         last = p;
-        const int l = p & 63;
-        const int r0 = __builtin_amdgcn_readlane(n0, l), r1 = __builtin_amdgcn_readlane(n1, l);
-        if (p < 64) {
-          cm0 |= 1ull << l;
-          p = r0;
-        } else {
-          cm1 |= 1ull << l;
-          p = r1;
-        }
+        cm0 |= 1ull << p;
+        p = __builtin_amdgcn_readlane(n0, p);
+      }
+      while (p < lim) {
+        last = p;
+        cm1 |= 1ull << (p - 64);
+        p = __builtin_amdgcn_readlane(n1, p - 64);
       }
       const bool on0 = (cm0 >> lane) & 1, on1 = (cm1 >> lane) & 1;
       PQG_ST(tc);

@@ -382,6 +382,7 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
                                                const RunEnt* runs, const BlockDesc* blks) {
   __shared__ __attribute__((aligned(16))) ValuesShared sh;
   const int lane = lane_id();
+  if (total[kModePresentOff + Mode] == 0) return;  // no page of this stage
   for (;;) {
     PQG_T(tp0);
     const int t = queue_next(queue);
@@ -414,7 +415,7 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
         dict_w = val[0];
         if (dict_w > 32) re = kBIT_WIDTH;
       }
-    } else if (Mode == 0 && enc == 5) {
+    } else if (Mode == 3 && enc == 5) {
       re = dbp_decode(val, vn, readable, job.type == 2, 0, nullptr, sh.dbp, 0);
     } else if (Mode == 0 && enc == 3 && job.type == 0) {
       if (vn < 4) re = kEOF;
@@ -479,7 +480,7 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
         if (bad < nn && (serr == kOK || bad < S.produced)) de = kDICT_INDEX;
         else de = serr;
       }
-    } else if (Mode == 0 && enc == 5) {
+    } else if (Mode == 3 && enc == 5) {
       de = dbp_decode(val, vn, readable, job.type == 2, nn, out, sh.dbp, 1);
     } else if (Mode == 0 && enc == 3 && job.type == 0) {  // booleanRLEDecoder: hybrid w=1 after a u32 length
       const HStream S = streams[pg.hs_val];
@@ -498,6 +499,8 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
 template __global__ void k_values<0>(JobDev*, PageDev*, const int*, const int*, int*, uint8_t*, const HStream*,
                                     const RunEnt*, const BlockDesc*);
 template __global__ void k_values<1>(JobDev*, PageDev*, const int*, const int*, int*, uint8_t*, const HStream*,
+                                    const RunEnt*, const BlockDesc*);
+template __global__ void k_values<3>(JobDev*, PageDev*, const int*, const int*, int*, uint8_t*, const HStream*,
                                     const RunEnt*, const BlockDesc*);
 
 // ============================================================================
