@@ -27,7 +27,10 @@
 
 namespace pqg {
 
-constexpr int kGroup = 4;  // blocks per expander step
+#ifndef PQG_KGROUP
+#define PQG_KGROUP 2
+#endif
+constexpr int kGroup = PQG_KGROUP;  // blocks per expander step
 
 struct ExpandShared {
   BlockDesc desc[64];
@@ -136,8 +139,13 @@ __device__ __forceinline__ void block_values_1(const ExpandShared& sh, int b, co
 }
 
 // Sink:
-//   void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup], const int (&cnt)[kGroup])
+//   void prepare(v, i0, cnt)  issue the group's loads (dictionary gathers), or nothing
+//   void group(v, i0, cnt)    consume them and store
 // values v[b][0..cnt[b]) belong at value indices i0[b]...; cnt[b] == 0: none.
+// Between the two calls the expander issues the next group's run/payload
+// loads, so that (vmcnt retires in issue order) the wait for the gathers
+// never includes those loads, the wait for those loads never includes this
+// group's stores, and the gather and payload latencies overlap.
 template <class Sink>
 __device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __restrict__ runs_,
                                               const BlockDesc* __restrict__ blks_, int64_t count, ExpandShared& sh,
@@ -175,23 +183,32 @@ __device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __
       const uint32_t nv0 = blks[b0 + nb].v0;
       tail_end = nv0 < end_all ? nv0 : end_all;
     }
-    for (int k0 = 0; k0 < nk; k0 += kGroup) {
-      PQG_T(t0);
-      BlockGeom g[kGroup];
-      uint32_t rs[kGroup], rv[kGroup];
-      uint4 gr[kGroup];
+    // every lane issues, for each block of group k0, the load of one run entry
+    // and one 16-byte payload granule (unconditionally: a guarded load is
+    // merged with the register's old value at the branch join, and that copy
+    // waits for the load on the spot)
+    uint32_t rs[kGroup], rv[kGroup];
+    uint4 gr[kGroup];
+    auto issue = [&](int k0) {
 #pragma unroll
       for (int b = 0; b < kGroup; b++) {
         const int k = k0 + b < nk ? k0 + b : nk - 1;  // past the end: repeat the last block, unused
-        g[b] = block_geom(sh, k, nk, tail_end, pa);
-        const uint32_t ri = (uint32_t)lane < g[b].nr ? (uint32_t)lane : 0u;  // nr >= 1
-        rs[b] = runs[g[b].r0 + ri].start;
-        rv[b] = runs[g[b].r0 + ri].src;
+        const BlockGeom g = block_geom(sh, k, nk, tail_end, pa);
+        const uint32_t ri = (uint32_t)lane < g.nr ? (uint32_t)lane : 0u;  // nr >= 1
+        rs[b] = runs[g.r0 + ri].start;
+        rv[b] = runs[g.r0 + ri].src;
         // granule `lane`, if it holds a stream byte < n (mapped); else a safe address
-        const int64_t at = g[b].sb + 16 * lane;
-        const bool want = lane < g[b].ng && at < n;
-        gr[b] = ldg16(want ? (uintptr_t)(sp + at) : ((uintptr_t)(runs + g[b].r0) & ~(uintptr_t)15));
+        const int64_t at = g.sb + 16 * lane;
+        const bool want = lane < g.ng && at < n;
+        gr[b] = ldg16(want ? (uintptr_t)(sp + at) : ((uintptr_t)(runs + g.r0) & ~(uintptr_t)15));
       }
+    };
+    issue(0);
+    for (int k0 = 0; k0 < nk; k0 += kGroup) {
+      PQG_T(t0);
+      BlockGeom g[kGroup];
+#pragma unroll
+      for (int b = 0; b < kGroup; b++) g[b] = block_geom(sh, k0 + b < nk ? k0 + b : nk - 1, nk, tail_end, pa);
       PQG_T(t1);
       PQG_ACC(0, t0, t1);
       __builtin_amdgcn_wave_barrier();
@@ -205,10 +222,13 @@ __device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __
         if (lane < g[b].ng) sts16(lds_ptr(sh.stage[b]) + 4 * lane, mask_tail(gr[b], g[b].sb + 16 * lane, n));
       }
       __builtin_amdgcn_wave_barrier();
+      uint32_t s0[kGroup], src0[kGroup];
 #pragma unroll
       for (int b = 0; b < kGroup; b++) {
         // run r > 0 starts inside the block (run 0 holds value v0)
         if (lane > 0 && (uint32_t)lane < g[b].nr) sh.rmap[b][(rs[b] & ~kRunBP) - g[b].v0] = (uint8_t)lane;
+        s0[b] = (uint32_t)__builtin_amdgcn_readfirstlane(rs[b]);
+        src0[b] = (uint32_t)__builtin_amdgcn_readfirstlane(rv[b]);
       }
       __builtin_amdgcn_wave_barrier();
       PQG_T(t2);
@@ -220,13 +240,14 @@ __device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __
         i0[b] = g[b].v0 + lane * 8;
         cnt[b] = (k0 + b < nk && i0[b] < g[b].v1) ? (int)(g[b].v1 - i0[b] < 8 ? g[b].v1 - i0[b] : 8) : 0;
         if (g[b].nr == 1)
-          block_values_1(sh, b, g[b], (uint32_t)__builtin_amdgcn_readfirstlane(rs[b]),
-                         (uint32_t)__builtin_amdgcn_readfirstlane(rv[b]), mask, w, lane, v[b]);
+          block_values_1(sh, b, g[b], s0[b], src0[b], mask, w, lane, v[b]);
         else
           block_values(sh, b, g[b], mask, w, lane, v[b]);
       }
       PQG_T(t3);
       PQG_ACC(2, t2, t3);
+      sink.prepare(v, i0, cnt);
+      if (k0 + kGroup < nk) issue(k0 + kGroup);  // the next group's loads, under the gathers
       sink.group(v, i0, cnt);
       PQG_T(t4);
       PQG_ACC(3, t3, t4);

@@ -345,6 +345,7 @@ struct StrDictCount {
   int64_t count;
   int64_t bad;   // first value index with an invalid key
   int64_t sum;   // lane's chars
+  __device__ __forceinline__ void prepare(const uint32_t (&)[kGroup][8], const uint32_t (&)[kGroup], const int (&)[kGroup]) {}
   __device__ __forceinline__ void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup],
                                         const int (&cnt)[kGroup]) {
 #pragma unroll

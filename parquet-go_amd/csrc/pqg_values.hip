@@ -41,39 +41,46 @@ struct DictSink {
   int64_t bad;      // first index with an invalid key
   int64_t nil_key;  // INT96 partial final entry (-1: none): its value reads as zero bytes (Q8)
   int w;
+  // W == 4, every key of the group valid (checked with one max + one ballot
+  // instead of per value): the gathers issued by prepare(), stored by group()
+  bool fast = false;
+  uint32_t gv4[kGroup][8];
+  __device__ __forceinline__ void prepare(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup],
+                                          const int (&cnt)[kGroup]) {
+    if (W != 4) return;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int b = 0; b < kGroup; b++)
+#pragma unroll
+      for (int q = 0; q < 8; q++) mx = q < cnt[b] && v[b][q] > mx ? v[b][q] : mx;
+    fast = !__ballot((int64_t)mx >= count);
+    if (!fast) return;
+    const PQG_G uint32_t* d = (const PQG_G uint32_t*)dict;
+#pragma unroll
+    for (int b = 0; b < kGroup; b++)
+#pragma unroll
+      for (int q = 0; q < 8; q++) gv4[b][q] = d[q < cnt[b] ? v[b][q] : 0u];
+  }
   __device__ __forceinline__ void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup],
                                         const int (&cnt)[kGroup]) {
-    if (W == 4) {
-      // common case: every key of the group is valid (one max + one ballot
-      // instead of a check per value)
-      uint32_t mx = 0;
+    if (W == 4 && fast) {
 #pragma unroll
-      for (int b = 0; b < kGroup; b++)
+      for (int b = 0; b < kGroup; b++) {
+        if (cnt[b] == 0) continue;
+        const uintptr_t o = (uintptr_t)(out + (int64_t)i0[b] * 4);
+        if (cnt[b] == 8 && (o & 15) == 0) {
+          stg16(o, make_uint4(gv4[b][0], gv4[b][1], gv4[b][2], gv4[b][3]));
+          stg16(o + 16, make_uint4(gv4[b][4], gv4[b][5], gv4[b][6], gv4[b][7]));
+        } else if (cnt[b] == 8 && (o & 7) == 0) {
 #pragma unroll
-        for (int q = 0; q < 8; q++) mx = q < cnt[b] && v[b][q] > mx ? v[b][q] : mx;
-      if (!__ballot((int64_t)mx >= count)) {
-        uint32_t gv[kGroup][8];
-        const PQG_G uint32_t* d = (const PQG_G uint32_t*)dict;
+          for (int q = 0; q < 8; q += 2) stg8(o + 4 * q, gv4[b][q], gv4[b][q + 1]);
+        } else {
 #pragma unroll
-        for (int b = 0; b < kGroup; b++)
-#pragma unroll
-          for (int q = 0; q < 8; q++) gv[b][q] = d[q < cnt[b] ? v[b][q] : 0u];
-#pragma unroll
-        for (int b = 0; b < kGroup; b++) {
-          if (cnt[b] == 0) continue;
-          const uintptr_t o = (uintptr_t)(out + (int64_t)i0[b] * 4);
-          if (cnt[b] == 8 && (o & 15) == 0) {
-            stg16(o, make_uint4(gv[b][0], gv[b][1], gv[b][2], gv[b][3]));
-            stg16(o + 16, make_uint4(gv[b][4], gv[b][5], gv[b][6], gv[b][7]));
-          } else if (cnt[b] == 8 && (o & 7) == 0) {
-#pragma unroll
-            for (int q = 0; q < 8; q += 2) stg8(o + 4 * q, gv[b][q], gv[b][q + 1]);
-          } else {
-            for (int q = 0; q < cnt[b]; q++) ((PQG_G uint32_t*)o)[q] = gv[b][q];
-          }
+          for (int q = 0; q < 8; q++)  // constant indices: the values stay in registers
+            if (q < cnt[b]) ((PQG_G uint32_t*)o)[q] = gv4[b][q];
         }
-        return;
       }
+      return;
     }
     bool ok[kGroup][8];
 #pragma unroll
@@ -99,7 +106,8 @@ struct DictSink {
           stg16(o, make_uint4(gv[b][0], gv[b][1], gv[b][2], gv[b][3]));
           stg16(o + 16, make_uint4(gv[b][4], gv[b][5], gv[b][6], gv[b][7]));
         } else {
-          for (int q = 0; q < cnt[b]; q++)
+#pragma unroll
+          for (int q = 0; q < 8; q++)
             if (ok[b][q]) ((PQG_G uint32_t*)o)[q] = gv[b][q];
         }
       }
@@ -114,12 +122,15 @@ struct DictSink {
       for (int b = 0; b < kGroup; b++) {
         if (cnt[b] == 0) continue;
         const uintptr_t o = (uintptr_t)(out + (int64_t)i0[b] * 8);
-        for (int q = 0; q < cnt[b]; q++)
+#pragma unroll
+        for (int q = 0; q < 8; q++)
           if (ok[b][q]) stg8(o + 8 * q, gv[b][q].x, gv[b][q].y);
       }
     } else {
+#pragma unroll
       for (int b = 0; b < kGroup; b++)
-        for (int q = 0; q < cnt[b]; q++) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
           if (!ok[b][q]) continue;
           const int64_t key = v[b][q], i = (int64_t)i0[b] + q;
           gcu8 s = dict + key * w;
@@ -132,6 +143,7 @@ struct DictSink {
 // booleanRLEDecoder (type_boolean.go:100-120): value == 1
 struct BoolSink {
   gu8 out;
+  __device__ __forceinline__ void prepare(const uint32_t (&)[kGroup][8], const uint32_t (&)[kGroup], const int (&)[kGroup]) {}
   __device__ __forceinline__ void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup],
                                         const int (&cnt)[kGroup]) {
     for (int b = 0; b < kGroup; b++)
@@ -409,7 +421,7 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
     // ---- valuesDecoder.init (read phase)
     int re = kOK;
     int dict_w = 0;
-    if (enc == 8) {
+    if ((Mode == 0 || Mode == 1) && enc == 8) {
       if (vn < 1) re = kEOF;
       else {
         dict_w = val[0];
@@ -448,7 +460,7 @@ __global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, con
       } else {
         de = kUNSUPPORTED;  // variable length: pqg_strings.hip
       }
-    } else if (enc == 8) {
+    } else if ((Mode == 0 || Mode == 1) && enc == 8) {
       const gcu8 dict = gconst(job.dict_data);
       const int64_t dcount = job.dict_data ? job.dict_count : 0;
       const int64_t nil_key = (job.flags & 1) ? dcount - 1 : -1;
