@@ -56,28 +56,72 @@ struct DictSink {
     fast = !__ballot((int64_t)mx >= count);
     if (!fast) return;
     const PQG_G uint32_t* d = (const PQG_G uint32_t*)dict;
+#ifdef PQG_EXP_NOGATHER
+#pragma unroll
+    for (int b = 0; b < kGroup; b++)
+#pragma unroll
+      for (int q = 0; q < 8; q++) gv4[b][q] = v[b][q];
+    (void)d;
+#else
 #pragma unroll
     for (int b = 0; b < kGroup; b++)
 #pragma unroll
       for (int q = 0; q < 8; q++) gv4[b][q] = d[q < cnt[b] ? v[b][q] : 0u];
+#endif
   }
   __device__ __forceinline__ void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup],
                                         const int (&cnt)[kGroup]) {
     if (W == 4 && fast) {
+#ifdef PQG_EXP_NOSTORE
+      uint32_t x = 0;
+#pragma unroll
+      for (int b = 0; b < kGroup; b++)
+#pragma unroll
+        for (int q = 0; q < 8; q++) x ^= gv4[b][q];
+      if (x == 0x9e3779b9u) *(PQG_G uint32_t*)out = x;  // keeps the gathers alive
+      return;
+#endif
+      // Aligned 16-byte stores whatever the page's alignment: the block's
+      // values start s elements before a 16-byte boundary, so lane L stores
+      // the 8 values [8L + s, 8L + s + 8) — its own from s on and the first s
+      // of lane L + 1 (DPP wave_shl:1) — as two aligned granules; lane 0
+      // stores the block's first s values, and ragged lanes store per value.
+      const int lane = lane_id();
 #pragma unroll
       for (int b = 0; b < kGroup; b++) {
-        if (cnt[b] == 0) continue;
-        const uintptr_t o = (uintptr_t)(out + (int64_t)i0[b] * 4);
-        if (cnt[b] == 8 && (o & 15) == 0) {
-          stg16(o, make_uint4(gv4[b][0], gv4[b][1], gv4[b][2], gv4[b][3]));
-          stg16(o + 16, make_uint4(gv4[b][4], gv4[b][5], gv4[b][6], gv4[b][7]));
-        } else if (cnt[b] == 8 && (o & 7) == 0) {
+        if (!__ballot(cnt[b] > 0)) continue;
+        const uint32_t v0 = (uint32_t)__builtin_amdgcn_readfirstlane(i0[b]);
+        const uintptr_t base = (uintptr_t)(out + (int64_t)v0 * 4);
+        const int sh_ = (int)(((16 - (base & 15)) & 15) >> 2);
+        const int s = __builtin_amdgcn_readfirstlane(sh_);
+        uint32_t nx[3];
 #pragma unroll
-          for (int q = 0; q < 8; q += 2) stg8(o + 4 * q, gv4[b][q], gv4[b][q + 1]);
+        for (int q = 0; q < 3; q++) nx[q] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)gv4[b][q], 0x130, 0xf, 0xf, true);
+        const int nxc = __builtin_amdgcn_update_dpp(0, cnt[b], 0x130, 0xf, 0xf, true);
+        uint32_t w[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          // w[q] = value 8L + s + q
+          const uint32_t a1 = q + 1 < 8 ? gv4[b][q + 1] : nx[0];
+          const uint32_t a2 = q + 2 < 8 ? gv4[b][q + 2] : nx[q + 2 - 8];
+          const uint32_t a3 = q + 3 < 8 ? gv4[b][q + 3] : nx[q + 3 - 8];
+          w[q] = s == 0 ? gv4[b][q] : s == 1 ? a1 : s == 2 ? a2 : a3;
+        }
+        const uintptr_t o = base + 32 * (uintptr_t)lane + 4 * (uintptr_t)s;
+        if (cnt[b] == 8 && nxc >= s) {
+          stg16(o, make_uint4(w[0], w[1], w[2], w[3]));
+          stg16(o + 16, make_uint4(w[4], w[5], w[6], w[7]));
         } else {
 #pragma unroll
-          for (int q = 0; q < 8; q++)  // constant indices: the values stay in registers
-            if (q < cnt[b]) ((PQG_G uint32_t*)o)[q] = gv4[b][q];
+          for (int q = 0; q < 8; q++) {
+            const int r = s + q;
+            if (r < 8 ? r < cnt[b] : r - 8 < nxc) *(PQG_G uint32_t*)(o + 4 * q) = w[q];
+          }
+        }
+        if (lane == 0) {
+#pragma unroll
+          for (int q = 0; q < 3; q++)
+            if (q < s && q < cnt[b]) *(PQG_G uint32_t*)(base + 4 * q) = gv4[b][q];
         }
       }
       return;
