@@ -148,6 +148,50 @@ __device__ __forceinline__ uint64_t extract_bits64(P p, int64_t n, int64_t valid
 }
 
 // ---------------------------------------------------------------------------
+// Lane-contiguous output runs as aligned 16-byte stores: lane L's D dwords go
+// to base + 4 (D L + i), i < nv (nv = D except at the ragged end; base is
+// 4-byte aligned).  The run starts s dwords before a 16-byte boundary, so lane
+// L stores dwords [D L + s, D L + s + D) — its own from s on and the first s
+// of lane L + 1 (DPP wave_shl:1) — as aligned granules; lane 0 stores the
+// first s dwords and ragged lanes store per dword.  All 64 lanes must be
+// active.
+// ---------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ void store_run_aligned(uintptr_t base, const uint32_t (&d)[D], int nv) {
+  static_assert(D % 4 == 0, "whole granules per lane");
+  const int lane = lane_id();
+  const int s = __builtin_amdgcn_readfirstlane((int)(((16 - (base & 15)) & 15) >> 2));
+  uint32_t nx[3];
+#pragma unroll
+  for (int q = 0; q < 3; q++) nx[q] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d[q], 0x130, 0xf, 0xf, true);
+  const int nxv = __builtin_amdgcn_update_dpp(0, nv, 0x130, 0xf, 0xf, true);
+  uint32_t w[D];
+#pragma unroll
+  for (int q = 0; q < D; q++) {
+    const uint32_t a1 = q + 1 < D ? d[q + 1] : nx[q + 1 - D];
+    const uint32_t a2 = q + 2 < D ? d[q + 2] : nx[q + 2 - D];
+    const uint32_t a3 = q + 3 < D ? d[q + 3] : nx[q + 3 - D];
+    w[q] = s == 0 ? d[q] : s == 1 ? a1 : s == 2 ? a2 : a3;
+  }
+  const uintptr_t o = base + 4 * ((uintptr_t)D * lane + s);
+  if (nv == D && nxv >= s) {
+#pragma unroll
+    for (int g = 0; g < D / 4; g++) stg16(o + 16 * g, make_uint4(w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]));
+  } else {
+#pragma unroll
+    for (int q = 0; q < D; q++) {
+      const int r = s + q;
+      if (r < D ? r < nv : r - D < nxv) *(PQG_G uint32_t*)(o + 4 * q) = w[q];
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 3; q++)
+      if (q < s && q < nv) *(PQG_G uint32_t*)(base + 4 * q) = d[q];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Wave-cooperative byte copy, any alignment on either side: 16-byte aligned
 // destination granules (one dwordx4 store per lane), each funnel-shifted out of
 // two aligned 16-byte source granules; ragged head and tail bytewise.  Only

@@ -81,48 +81,12 @@ struct DictSink {
       if (x == 0x9e3779b9u) *(PQG_G uint32_t*)out = x;  // keeps the gathers alive
       return;
 #endif
-      // Aligned 16-byte stores whatever the page's alignment: the block's
-      // values start s elements before a 16-byte boundary, so lane L stores
-      // the 8 values [8L + s, 8L + s + 8) — its own from s on and the first s
-      // of lane L + 1 (DPP wave_shl:1) — as two aligned granules; lane 0
-      // stores the block's first s values, and ragged lanes store per value.
-      const int lane = lane_id();
+      // aligned 16-byte stores whatever the page's alignment (store_run_aligned)
 #pragma unroll
       for (int b = 0; b < kGroup; b++) {
         if (!__ballot(cnt[b] > 0)) continue;
         const uint32_t v0 = (uint32_t)__builtin_amdgcn_readfirstlane(i0[b]);
-        const uintptr_t base = (uintptr_t)(out + (int64_t)v0 * 4);
-        const int sh_ = (int)(((16 - (base & 15)) & 15) >> 2);
-        const int s = __builtin_amdgcn_readfirstlane(sh_);
-        uint32_t nx[3];
-#pragma unroll
-        for (int q = 0; q < 3; q++) nx[q] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)gv4[b][q], 0x130, 0xf, 0xf, true);
-        const int nxc = __builtin_amdgcn_update_dpp(0, cnt[b], 0x130, 0xf, 0xf, true);
-        uint32_t w[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          // w[q] = value 8L + s + q
-          const uint32_t a1 = q + 1 < 8 ? gv4[b][q + 1] : nx[0];
-          const uint32_t a2 = q + 2 < 8 ? gv4[b][q + 2] : nx[q + 2 - 8];
-          const uint32_t a3 = q + 3 < 8 ? gv4[b][q + 3] : nx[q + 3 - 8];
-          w[q] = s == 0 ? gv4[b][q] : s == 1 ? a1 : s == 2 ? a2 : a3;
-        }
-        const uintptr_t o = base + 32 * (uintptr_t)lane + 4 * (uintptr_t)s;
-        if (cnt[b] == 8 && nxc >= s) {
-          stg16(o, make_uint4(w[0], w[1], w[2], w[3]));
-          stg16(o + 16, make_uint4(w[4], w[5], w[6], w[7]));
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; q++) {
-            const int r = s + q;
-            if (r < 8 ? r < cnt[b] : r - 8 < nxc) *(PQG_G uint32_t*)(o + 4 * q) = w[q];
-          }
-        }
-        if (lane == 0) {
-#pragma unroll
-          for (int q = 0; q < 3; q++)
-            if (q < s && q < cnt[b]) *(PQG_G uint32_t*)(base + 4 * q) = gv4[b][q];
-        }
+        store_run_aligned<8>((uintptr_t)(out + (int64_t)v0 * 4), gv4[b], cnt[b]);
       }
       return;
     }
@@ -277,7 +241,9 @@ __device__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_
   }
   if (stage == 0) return kOK;
   const int64_t P = nn < total ? nn : total;  // positions actually produced before EOF
-  const bool regular = (mbvc % 8 == 0) && mbc <= kMaxMb;
+  const bool regular = (mbvc % 8 == 0) && mbc <= kMaxMb && bs <= (1 << 24);
+  const bool pow2 = (bs & (bs - 1)) == 0 && (mbvc & (mbvc - 1)) == 0;
+  const int bs_sh = __builtin_ctz((uint32_t)bs), mb_sh = __builtin_ctz((uint32_t)mbvc);
   if (!regular) {
     // ---- generic single-lane emulation of next() (rare layouts)
     int64_t rp = pos;
@@ -385,35 +351,57 @@ __device__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_
     }
     (void)first_block;
     __builtin_amdgcn_wave_barrier();
-    // unpack + wrapping prefix over positions [p0, p_end): value(p) = carry + Σ deltas
+    // unpack + wrapping prefix over positions [p0, p_end): value(p) = carry + Σ deltas.
+    // A lane's 4 positions share one miniblock (mbvc % 8 == 0), so the block /
+    // miniblock split is done once per lane, by shifts for power-of-two sizes.
     for (int64_t t0 = p0; t0 < p_end; t0 += 256) {
       uint64_t d[4];
       uint64_t local = 0;
+      const int64_t pb = t0 + lane * 4;
+      const uint32_t rel = (uint32_t)(pb - p0);  // < kBlocks * bs <= 2^31 (regular)
+      uint32_t b, r2, m, j;
+      if (pow2) {
+        b = rel >> bs_sh;
+        r2 = rel & (uint32_t)(bs - 1);
+        m = r2 >> mb_sh;
+        j = r2 & (uint32_t)(mbvc - 1);
+      } else {
+        b = rel / (uint32_t)bs;
+        r2 = rel - b * (uint32_t)bs;
+        m = r2 / (uint32_t)mbvc;
+        j = r2 - m * (uint32_t)mbvc;
+      }
+      const bool any = pb < p_end;
+      const int wv = any ? sh.widths[b][m] : 0;
+      const int64_t bit0 = any ? sh.mb_off[b][m] * 8 + (int64_t)j * wv : 0;
+      const uint64_t mnd = any ? sh.mind[b] : 0;
+#pragma unroll
       for (int k = 0; k < 4; k++) {
-        int64_t p = t0 + lane * 4 + k;
         uint64_t dv = 0;
-        if (p < p_end) {
-          int64_t rel = p - p0;
-          int b = (int)(rel / bs);
-          int64_t r2 = rel - (int64_t)b * bs;
-          int m = (int)(r2 / mbvc);
-          int64_t j = r2 - (int64_t)m * mbvc;
-          int wv = sh.widths[b][m];
-          uint64_t x = extract_bits64(s, readable, n, sh.mb_off[b][m] * 8 + j * wv, wv);
-          dv = x + sh.mind[b];
-        }
+        if (pb + k < p_end) dv = extract_bits64(s, readable, n, bit0 + (int64_t)k * wv, wv) + mnd;
         d[k] = dv;
         local += dv;
       }
       uint64_t incl = wave_incl_scan_u64(local);
       uint64_t run = carry + (incl - local);
-      for (int k = 0; k < 4; k++) {
-        int64_t p = t0 + lane * 4 + k;
-        if (p < p_end) {
-          if (is64) stg8((uintptr_t)(out + p * 8), (uint32_t)run, (uint32_t)(run >> 32));
-          else *(PQG_G uint32_t*)(out + p * 4) = (uint32_t)run;
+      const int nvp = pb >= p_end ? 0 : (p_end - pb >= 4 ? 4 : (int)(p_end - pb));
+      if (is64) {
+        uint32_t dw[8];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          dw[2 * k] = (uint32_t)run;
+          dw[2 * k + 1] = (uint32_t)(run >> 32);
+          run += d[k];
         }
-        run += d[k];
+        store_run_aligned<8>((uintptr_t)(out + t0 * 8), dw, 2 * nvp);
+      } else {
+        uint32_t dw[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          dw[k] = (uint32_t)run;
+          run += d[k];
+        }
+        store_run_aligned<4>((uintptr_t)(out + t0 * 4), dw, nvp);
       }
       carry += __shfl(incl, 63, 64);
     }
