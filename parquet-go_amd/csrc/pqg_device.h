@@ -156,7 +156,7 @@ __device__ __forceinline__ uint64_t extract_bits64(P p, int64_t n, int64_t valid
 // first s dwords and ragged lanes store per dword.  All 64 lanes must be
 // active.
 // ---------------------------------------------------------------------------
-template <int D>
+template <int D, bool NT = false>
 __device__ __forceinline__ void store_run_aligned(uintptr_t base, const uint32_t (&d)[D], int nv) {
   static_assert(D % 4 == 0, "whole granules per lane");
   const int lane = lane_id();
@@ -176,7 +176,14 @@ __device__ __forceinline__ void store_run_aligned(uintptr_t base, const uint32_t
   const uintptr_t o = base + 4 * ((uintptr_t)D * lane + s);
   if (nv == D && nxv >= s) {
 #pragma unroll
-    for (int g = 0; g < D / 4; g++) stg16(o + 16 * g, make_uint4(w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]));
+    for (int g = 0; g < D / 4; g++) {
+      if (NT) {
+        const u32x4_t v = {w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]};
+        __builtin_nontemporal_store(v, (PQG_G u32x4_t*)(o + 16 * g));
+      } else {
+        stg16(o + 16 * g, make_uint4(w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]));
+      }
+    }
   } else {
 #pragma unroll
     for (int q = 0; q < D; q++) {

@@ -166,12 +166,15 @@ struct GlobalSrc {
   bool hit;
   uintptr_t gaddr;  // 16-byte granule held in `g` (0: none)
   uint4 g;
+  const PQG_L uint8_t* win = nullptr;  // prefetched bytes [wlo, whi) (LDS), if any
+  int64_t wlo = 0, whi = 0;
   __device__ __forceinline__ int get(int64_t i) {
     if (i >= limit && i < n) {
       hit = true;
       return -1;
     }
     if (i < 0 || i >= n) return -1;
+    if (i >= wlo && i < whi) return win[i - wlo];
     const uintptr_t a = (uintptr_t)(p + i);
     const uintptr_t ga = a & ~(uintptr_t)15;
     if (ga != gaddr) {  // the granule holds byte i < n: mapped
@@ -193,10 +196,27 @@ constexpr int kCandFrames = 4, kCandLast = 8;
 
 // One lane parses and classifies the candidate at position p (kept out of
 // line: the scan loop around it must stay small).
+// The candidate's first bytes are prefetched into the lane's LDS window with
+// independent 16-byte loads (one memory round trip instead of one per granule
+// as the parser advances).
+constexpr int kCandWin = 5;  // granules: >= 64 bytes from any start
 __device__ __forceinline__ void parse_candidate(const JobDev& job, int64_t p, SkipFrame* frames, int16_t* lasts,
-                                             Cand* out) {
+                                             PQG_L uint8_t* win, Cand* out) {
   Compact<GlobalSrc> c;
   c.src = GlobalSrc{gconst(job.data), job.data_len, p + kCandParseBytes, false, 0, make_uint4(0, 0, 0, 0)};
+  {
+    const uintptr_t a0 = (uintptr_t)(job.data + p) & ~(uintptr_t)15;
+    const int64_t lo = p - (int64_t)((uintptr_t)(job.data + p) - a0);  // chunk offset of the first granule
+    uint4 g[kCandWin];
+#pragma unroll
+    for (int k = 0; k < kCandWin; k++)  // a granule holding a byte < n is mapped
+      g[k] = lo + 16 * k < job.data_len ? ldg16(a0 + 16 * k) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < kCandWin; k++) sts16(win + 16 * k, g[k]);
+    c.src.win = win;
+    c.src.wlo = lo;
+    c.src.whi = lo + 16 * kCandWin < job.data_len ? lo + 16 * kCandWin : job.data_len;
+  }
   // Structural pre-check: every thrift writer of PageHeader emits fields 1, 2,
   // 3 in id order with short-form i32 headers (15 t 15 <varint> 15).  A
   // candidate without that shape is not parsed: it is marked kCOMPLEX, which
@@ -339,6 +359,7 @@ __global__ void __launch_bounds__(256) k_cand_parse(JobDev* jobs, int n_jobs, co
                                                     const int64_t* cand_pos, Cand* cands) {
   __shared__ SkipFrame frames[256][kCandFrames];
   __shared__ int16_t lasts[256][kCandLast];
+  __shared__ __attribute__((aligned(16))) uint8_t wins[256][16 * kCandWin];
   int pre[kQShards + 1];  // the shards' list lengths, prefix-summed (uniform)
   pre[0] = 0;
 #pragma unroll
@@ -356,7 +377,7 @@ __global__ void __launch_bounds__(256) k_cand_parse(JobDev* jobs, int n_jobs, co
       if (jobs[mid].tile_base <= tile) lo = mid; else hi = mid - 1;
     }
     Cand* out = &cands[slot];
-    parse_candidate(jobs[lo], cand_pos[slot], frames[threadIdx.x], lasts[threadIdx.x], out);
+    parse_candidate(jobs[lo], cand_pos[slot], frames[threadIdx.x], lasts[threadIdx.x], lds_ptr(wins[threadIdx.x]), out);
     if (out->status == kOK) atomicAdd(&tile_okc[tile], 1);
   }
 }

@@ -86,7 +86,11 @@ struct DictSink {
       for (int b = 0; b < kGroup; b++) {
         if (!__ballot(cnt[b] > 0)) continue;
         const uint32_t v0 = (uint32_t)__builtin_amdgcn_readfirstlane(i0[b]);
-        store_run_aligned<8>((uintptr_t)(out + (int64_t)v0 * 4), gv4[b], cnt[b]);
+        // dictionaries larger than 256 KiB: non-temporal stores keep the
+        // output from evicting dictionary lines (b = 20: -5 %)
+        if (count > 65536) store_run_aligned<8, true>((uintptr_t)(out + (int64_t)v0 * 4), gv4[b], cnt[b]);
+        else
+          store_run_aligned<8>((uintptr_t)(out + (int64_t)v0 * 4), gv4[b], cnt[b]);
       }
       return;
     }
