@@ -23,6 +23,10 @@
 
 namespace pqg {
 
+#ifndef PQG_LEVELS_WPE
+#define PQG_LEVELS_WPE 6  // minimum waves per SIMD the register allocation must allow
+#endif
+
 #ifdef PQG_PROFILE
 // host reader of this translation unit's phase counters (see pqg_debug_counters)
 int prof_read_levels(unsigned long long* out) {
@@ -841,7 +845,7 @@ __device__ __forceinline__ int level_stream(gcu8 p, int64_t n, int w, uint32_t c
 // Setup (the read phase of the page, as k_page_setup) and the level decode
 // (as k_levels_expand) of one data page per wave; the value streams are
 // registered for the walker.
-__global__ void __launch_bounds__(64) k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+__global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total,
                                                     int* queue, uint8_t* scratch, HStream* streams,
                                                     uint8_t* def_arena, uint8_t* rep_arena) {
   __shared__ __attribute__((aligned(16))) LevShared sh;

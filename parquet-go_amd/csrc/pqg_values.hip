@@ -16,6 +16,13 @@
 
 namespace pqg {
 
+#ifndef PQG_DBP_WPE
+#define PQG_DBP_WPE 4  // the same for the DELTA_BINARY_PACKED stage
+#endif
+#ifndef PQG_VALUES_WPE
+#define PQG_VALUES_WPE 1  // minimum waves per SIMD the register allocation must allow
+#endif
+
 #ifdef PQG_PROFILE
 // host reader of this translation unit's phase counters (see pqg_debug_counters)
 int prof_read_values(unsigned long long* out) {
@@ -425,7 +432,7 @@ union ValuesShared {
 // apart so that its register budget is not the union of every encoding's);
 // mode 0: every other data page.  k_page_setup builds the two page lists.
 template <int Mode>
-__global__ void __launch_bounds__(64) k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+__global__ void __launch_bounds__(64, Mode == 3 ? PQG_DBP_WPE : PQG_VALUES_WPE) k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total,
                                                int* queue, uint8_t* value_arena, const HStream* streams,
                                                const RunEnt* runs, const BlockDesc* blks) {
   __shared__ __attribute__((aligned(16))) ValuesShared sh;
