@@ -197,9 +197,12 @@ constexpr int kCandFrames = 4, kCandLast = 8;
 // One lane parses and classifies the candidate at position p (kept out of
 // line: the scan loop around it must stay small).
 // The candidate's first bytes are prefetched into the lane's LDS window with
-// independent 16-byte loads (one memory round trip instead of one per granule
-// as the parser advances).
-constexpr int kCandWin = 5;  // granules: >= 64 bytes from any start
+// independent 16-byte loads, and the parse is confined to them: a header that
+// does not end inside the window is kCOMPLEX (its chunk takes the serial walk
+// only if a page link lands on it).  Without the bound, the slowest candidate
+// — garbage that passes the pre-check and reads on through the chunk one
+// dependent granule load at a time — set the kernel's time.
+constexpr int kCandWin = 10;  // granules: >= 144 bytes from any start
 __device__ __forceinline__ void parse_candidate(const JobDev& job, int64_t p, SkipFrame* frames, int16_t* lasts,
                                              PQG_L uint8_t* win, Cand* out) {
   Compact<GlobalSrc> c;
@@ -216,6 +219,7 @@ __device__ __forceinline__ void parse_candidate(const JobDev& job, int64_t p, Sk
     c.src.win = win;
     c.src.wlo = lo;
     c.src.whi = lo + 16 * kCandWin < job.data_len ? lo + 16 * kCandWin : job.data_len;
+    if (c.src.whi < c.src.limit) c.src.limit = c.src.whi;
   }
   // Structural pre-check: every thrift writer of PageHeader emits fields 1, 2,
   // 3 in id order with short-form i32 headers (15 t 15 <varint> 15).  A
