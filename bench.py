@@ -255,7 +255,7 @@ def cpu_baseline(wl, seconds):
 
 
 # ---------------------------------------------------------------- PMC traffic (committed passes)
-STAGE_KERNELS = {"scan": ["k_page_cands", "k_cand_parse", "k_tile_scan", "k_cand_link", "k_page_chain",
+STAGE_KERNELS = {"scan": ["k_tile_jobs", "k_page_cands", "k_cand_parse", "k_tile_scan", "k_cand_link", "k_page_chain",
                           "k_scan_pages"], "list": ["k_page_list"], "snappy": ["k_snappy"], "levels": ["k_page_levels"],
                  "walk": ["k_hybrid_walk"], "unused": [], "nn_scan": ["k_nn_scan"],
                  "values": ["k_values"], "strings": ["k_str_dict", "k_str_plain", "k_str_count", "k_char_scan",

@@ -25,13 +25,14 @@ int pack_levels_launch(hipStream_t s, const uint8_t* levels, int64_t n, int bw, 
 }
 
 namespace pqg {
-__global__ void k_page_cands(JobDev* jobs, int n_jobs, int* tile_count, int* tile_okc, int64_t* cand_pos,
+__global__ void k_tile_jobs(const JobDev* jobs, int* tile_job);
+__global__ void k_page_cands(JobDev* jobs, const int* tile_job, int* tile_count, int* tile_okc, int64_t* cand_pos,
                              int* cand_list, int* cand_total, int region);
-__global__ void k_cand_parse(JobDev* jobs, int n_jobs, const int* cand_list, const int* cand_total, int region,
+__global__ void k_cand_parse(JobDev* jobs, const int* tile_job, const int* cand_list, const int* cand_total, int region,
                              int* tile_okc,
                              const int64_t* cand_pos, Cand* cands);
 __global__ void k_tile_scan(JobDev* jobs, const int* tile_count, const int* tile_okc, int* tile_off, int* tile_okoff);
-__global__ void k_cand_link(JobDev* jobs, int n_jobs, int64_t total_tiles, const int* tile_count,
+__global__ void k_cand_link(JobDev* jobs, const int* tile_job, int64_t total_tiles, const int* tile_count,
                             const int* tile_off, const int* tile_okoff, const Cand* cands, int* succ, int* idx2slot,
                             int* ok2slot);
 __global__ void k_page_chain(JobDev* jobs, PageDev* pages, const Cand* cands, const int* succ,
@@ -137,6 +138,7 @@ struct pqg_ctx {
   int num_cus = 256;
   int snappy_per_cu = 2;  // resident k_snappy waves per CU (LDS-bound: the output history ring)
   DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
+  DevBuf tile_job;  // K1: tile -> job
   DevBuf tile_count, tile_okc, tile_off, tile_okoff, cand_pos, cands, succ, idx2slot, ok2slot, order;  // K1
   DevBuf streams, runs, blks;  // K3 hybrid run tables
   DevBuf cand_list, vlists;
@@ -221,7 +223,7 @@ void pqg_ctx_destroy(pqg_ctx* c) {
   for (DevBuf* b : {&c->jobs, &c->pages, &c->list, &c->counters, &c->def_arena, &c->rep_arena, &c->value_arena,
                     &c->scratch, &c->streams, &c->runs, &c->blks, &c->cand_list, &c->vlists, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
                     &c->ok2slot, &c->order, &c->asm_seg, &c->offs_arena, &c->doffs_arena, &c->page_stage,
-                    &c->blk_src, &c->blk_dst, &c->blk_meta})
+                    &c->blk_src, &c->blk_dst, &c->blk_meta, &c->tile_job})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
   hipStreamDestroy(c->stream);
@@ -344,7 +346,7 @@ static int plan_batch(pqg_ctx* c) {
       c->rep_arena.grow((size_t)slot_total + 64) || c->value_arena.grow((size_t)value_total + 64) ||
       c->scratch.grow((size_t)scratch_total + 64) || c->tile_count.grow(sizeof(int) * (size_t)tile_total + 64) ||
       c->tile_off.grow(sizeof(int) * (size_t)tile_total + 64) || c->tile_okc.grow(sizeof(int) * (size_t)tile_total + 64) ||
-      c->tile_okoff.grow(sizeof(int) * (size_t)tile_total + 64) ||
+      c->tile_okoff.grow(sizeof(int) * (size_t)tile_total + 64) || c->tile_job.grow(sizeof(int) * (size_t)tile_total + 64) ||
       c->ok2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->cand_pos.grow(sizeof(int64_t) * (size_t)tile_total * kCandPerTile + 64) ||
       c->cand_list.grow(sizeof(int) * (size_t)(tile_total + kQShards) * kCandPerTile + 64) ||
@@ -392,14 +394,17 @@ static int launch_pipeline(pqg_ctx* c) {
     int64_t* cpos = (int64_t*)c->cand_pos.p;
     int* clist = (int*)c->cand_list.p;
     const int region = (int)((nt + kQShards - 1) / kQShards) * kCandPerTile;  // one list region per head
-    hipLaunchKernelGGL(k_page_cands, dim3((unsigned)nt), dim3(256), 0, s, jobs, n, tcount, tokc, cpos, clist, Q(7),
+    hipLaunchKernelGGL(k_tile_jobs, dim3(n), dim3(256), 0, s, jobs, (int*)c->tile_job.p);
+    hipLaunchKernelGGL(k_page_cands, dim3((unsigned)nt), dim3(256), 0, s, jobs, (const int*)c->tile_job.p, tcount, tokc,
+                       cpos, clist, Q(7),
                        region);
     hipLaunchKernelGGL(k_cand_parse, dim3((unsigned)std::min<int64_t>((nt * kCandPerTile + 255) / 256, c->num_cus * 4)),
-                       dim3(256), 0, s, jobs, n, clist, Q(7), region, tokc, cpos, cands);
+                       dim3(256), 0, s, jobs, (const int*)c->tile_job.p, clist, Q(7), region, tokc, cpos, cands);
   }
   hipLaunchKernelGGL(k_tile_scan, dim3(n), dim3(1024), 0, s, jobs, tcount, tokc, toff, tokoff);
   if (nt > 0)
-    hipLaunchKernelGGL(k_cand_link, dim3((unsigned)((nt * kCandPerTile + 255) / 256)), dim3(256), 0, s, jobs, n, nt,
+    hipLaunchKernelGGL(k_cand_link, dim3((unsigned)((nt * kCandPerTile + 255) / 256)), dim3(256), 0, s, jobs,
+                       (const int*)c->tile_job.p, nt,
                        tcount, toff, tokoff, cands, (int*)c->succ.p, (int*)c->idx2slot.p, (int*)c->ok2slot.p);
   hipLaunchKernelGGL(k_page_chain, dim3(n), dim3(1024), 0, s, jobs, pages, cands, (const int*)c->succ.p,
                      (const int*)c->idx2slot.p, (const int*)c->ok2slot.p, (int*)c->order.p);

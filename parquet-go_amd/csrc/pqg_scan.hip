@@ -277,7 +277,14 @@ __device__ __forceinline__ void parse_candidate(const JobDev& job, int64_t p, Sk
 // cand_total: kQShards counters kQStride ints apart; tile t appends to shard
 // t & 7, whose list region starts at (t & 7) * region (a single list head
 // would take one contended device-scope atomic per tile).
-__global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, int n_jobs, int* tile_count, int* tile_okc,
+// tile -> job map (one block per job): the scan kernels look a tile's job up
+// with one load instead of a binary search over the job table.
+__global__ void __launch_bounds__(256) k_tile_jobs(const JobDev* jobs, int* tile_job) {
+  const JobDev& job = jobs[blockIdx.x];
+  for (int64_t t = threadIdx.x; t < job.n_tiles; t += 256) tile_job[job.tile_base + t] = (int)blockIdx.x;
+}
+
+__global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, const int* tile_job, int* tile_count, int* tile_okc,
                                                     int64_t* cand_pos, int* cand_list, int* cand_total, int region) {
   __shared__ int cnt;
   __shared__ int job_s;
@@ -286,12 +293,7 @@ __global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, int n_jobs, in
   const int64_t tile = blockIdx.x;
   if (tid == 0) {
     cnt = 0;
-    int lo = 0, hi = n_jobs - 1;  // last job with tile_base <= tile
-    while (lo < hi) {
-      int mid = (lo + hi + 1) >> 1;
-      if (jobs[mid].tile_base <= tile) lo = mid; else hi = mid - 1;
-    }
-    job_s = lo;
+    job_s = tile_job[tile];
   }
   __syncthreads();
   const JobDev& job = jobs[job_s];
@@ -358,7 +360,7 @@ __global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, int n_jobs, in
 // ---- K1a' ------------------------------------------------------------------
 // One lane per candidate slot: parse + classify (kept apart from the byte scan
 // so that the scan has no scratch and runs at full occupancy).
-__global__ void __launch_bounds__(256) k_cand_parse(JobDev* jobs, int n_jobs, const int* cand_list,
+__global__ void __launch_bounds__(256) k_cand_parse(JobDev* jobs, const int* tile_job, const int* cand_list,
                                                     const int* cand_total, int region, int* tile_okc,
                                                     const int64_t* cand_pos, Cand* cands) {
   __shared__ SkipFrame frames[256][kCandFrames];
@@ -375,11 +377,7 @@ __global__ void __launch_bounds__(256) k_cand_parse(JobDev* jobs, int n_jobs, co
     for (int k = 1; k < kQShards; k++) sh += i >= pre[k];
     const int slot = cand_list[sh * region + (i - pre[sh])];
     const int64_t tile = slot / kCandPerTile;
-    int lo = 0, hi = n_jobs - 1;
-    while (lo < hi) {
-      int mid = (lo + hi + 1) >> 1;
-      if (jobs[mid].tile_base <= tile) lo = mid; else hi = mid - 1;
-    }
+    const int lo = tile_job[tile];
     Cand* out = &cands[slot];
     parse_candidate(jobs[lo], cand_pos[slot], frames[threadIdx.x], lasts[threadIdx.x], lds_ptr(wins[threadIdx.x]), out);
     if (out->status == kOK) atomicAdd(&tile_okc[tile], 1);
@@ -442,7 +440,7 @@ constexpr int kSuccComplex = -4;  // candidate needs the serial parse
 // hits (`15 00 15 06 ..` inside a DataPageHeader), which fail to classify,
 // do not break the fast path: it checks that each ok candidate links to the
 // ok candidate of the next rank.
-__global__ void __launch_bounds__(256) k_cand_link(JobDev* jobs, int n_jobs, int64_t total_tiles,
+__global__ void __launch_bounds__(256) k_cand_link(JobDev* jobs, const int* tile_job, int64_t total_tiles,
                                                    const int* tile_count, const int* tile_off,
                                                    const int* tile_okoff, const Cand* cands, int* succ,
                                                    int* idx2slot, int* ok2slot) {
@@ -452,12 +450,7 @@ __global__ void __launch_bounds__(256) k_cand_link(JobDev* jobs, int n_jobs, int
   if (tile >= total_tiles) return;
   const int cntv = tile_count[tile];
   if (s >= cntv || cntv > kCandPerTile) return;
-  int lo = 0, hi = n_jobs - 1;
-  while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (jobs[mid].tile_base <= tile) lo = mid; else hi = mid - 1;
-  }
-  JobDev& job = jobs[lo];
+  JobDev& job = jobs[tile_job[tile]];
   if (job.scan_fallback) return;
   const Cand& cd = cands[tile * kCandPerTile + s];
   const int64_t tb = job.tile_base;
