@@ -303,12 +303,23 @@ __global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, const int* til
   const gcu8 base = gconst(job.data);
   const int64_t data_len = job.data_len;
   const uintptr_t a0 = (uintptr_t)(base + t0) & ~(uintptr_t)15;
-  for (int64_t off = (int64_t)tid * 16;; off += 256 * 16) {
-    const uintptr_t a = a0 + off;
+  // the tile's granules (<= 5 per thread: the tile start is aligned down) are
+  // all loaded before any is examined, so each thread keeps 80 bytes in flight
+  constexpr int kG = kScanTile / (256 * 16) + 1;
+  uint4 vv[kG];
+#pragma unroll
+  for (int it = 0; it < kG; it++) {
+    const uintptr_t a = a0 + (int64_t)tid * 16 + (int64_t)it * 256 * 16;
+    const int64_t p0 = (int64_t)(a - (uintptr_t)base);
+    // a granule holding a position < t1 <= data_len is mapped
+    vv[it] = p0 < t1 ? ldg16(a) : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int it = 0; it < kG; it++) {
+    const uintptr_t a = a0 + (int64_t)tid * 16 + (int64_t)it * 256 * 16;
     const int64_t p0 = (int64_t)(a - (uintptr_t)base);
     if (p0 >= t1) break;
-    // the 16-byte granule holds a position < t1 <= data_len, so it is mapped
-    const uint4 v = ldg16(a);
+    const uint4 v = vv[it];
     if (!(has_byte_15(v.x) || has_byte_15(v.y) || has_byte_15(v.z) || has_byte_15(v.w))) continue;
     // bytes 16, 17 (lookahead of the last two positions), read only when
     // byte 14 or 15 is 0x15; 0xff (no match) past the end of the buffer
