@@ -204,20 +204,33 @@ __device__ __forceinline__ void store_run_aligned(uintptr_t base, const uint32_t
 // two aligned 16-byte source granules; ragged head and tail bytewise.  Only
 // granules holding a source byte are read (mapped memory).
 // ---------------------------------------------------------------------------
+// Four granules per lane per step, every load issued before the first store
+// (one memory round trip per 4 KiB per wave instead of per 1 KiB).
 template <int Q>
 __device__ __forceinline__ void wave_copy_body(PQG_G uint8_t* db, uintptr_t sbase, uint32_t r, int64_t body) {
   const int lane = lane_id();
-  for (int64_t g = (int64_t)lane * 16; g < body; g += 64 * 16) {
-    const uint4 a = ldg16(sbase + g);
-    uint4 b = a;
-    if (Q != 0 || r != 0) b = ldg16(sbase + g + 16);
-    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    uint4 o;
-    o.x = __builtin_amdgcn_alignbit(w[Q + 1], w[Q], r);
-    o.y = __builtin_amdgcn_alignbit(w[Q + 2], w[Q + 1], r);
-    o.z = __builtin_amdgcn_alignbit(w[Q + 3], w[Q + 2], r);
-    o.w = __builtin_amdgcn_alignbit(w[Q + 4 < 8 ? Q + 4 : 7], w[Q + 3], r);
-    stg16((uintptr_t)(db + g), o);
+  constexpr int U = 4;
+  for (int64_t g0 = (int64_t)lane * 16; g0 < body; g0 += 64 * 16 * U) {
+    uint4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t g = g0 + (int64_t)u * 64 * 16;
+      const uintptr_t at = g < body ? sbase + g : sbase;  // sbase holds a source byte
+      a[u] = ldg16(at);
+      b[u] = (Q != 0 || r != 0) ? ldg16(g < body ? at + 16 : sbase) : a[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t g = g0 + (int64_t)u * 64 * 16;
+      if (g >= body) break;
+      const uint32_t w[8] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x, b[u].y, b[u].z, b[u].w};
+      uint4 o;
+      o.x = __builtin_amdgcn_alignbit(w[Q + 1], w[Q], r);
+      o.y = __builtin_amdgcn_alignbit(w[Q + 2], w[Q + 1], r);
+      o.z = __builtin_amdgcn_alignbit(w[Q + 3], w[Q + 2], r);
+      o.w = __builtin_amdgcn_alignbit(w[Q + 4 < 8 ? Q + 4 : 7], w[Q + 3], r);
+      stg16((uintptr_t)(db + g), o);
+    }
   }
 }
 
