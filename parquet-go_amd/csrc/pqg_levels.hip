@@ -984,18 +984,25 @@ __global__ void __launch_bounds__(256) k_nn_scan(JobDev* jobs, PageDev* pages, u
   JobDev& job = jobs[blockIdx.x];
   int np = job.num_pages < job.page_cap ? job.num_pages : job.page_cap;
   if (job.status == kCAPACITY) np = 0;
-  int64_t carry = 0;
-  for (int b = 0; b < np; b += 256) {
-    const int i = b + threadIdx.x;
-    int64_t v = 0;
-    if (i < np) {
-      const PageDev& pg = pages[job.page_base + i];
-      if (pg.page_type == 0 || pg.page_type == 3) v = pg.not_null;
-    }
-    int64_t tot;
-    const int64_t ex = block_excl_scan<256>(v, &tot, part);
-    if (i < np) pages[job.page_base + i].value_offset = carry + ex;
-    carry += tot;
+  // each thread takes a contiguous segment of pages: its loads are
+  // independent (one round trip per pass, not one per 256 pages), one block
+  // scan of the segment sums, then the offsets are written in a second pass
+  const int seg = (np + 255) / 256;
+  const int s0 = (int)threadIdx.x * seg, s1 = s0 + seg < np ? s0 + seg : np;
+  PageDev* pp = pages + job.page_base;
+  auto nn_of = [&](int i) -> int64_t {
+    const PageDev& pg = pp[i];
+    return (pg.page_type == 0 || pg.page_type == 3) ? (int64_t)pg.not_null : 0;
+  };
+  int64_t sum = 0;
+#pragma unroll 8
+  for (int i = s0; i < s1; i++) sum += nn_of(i);
+  int64_t carry;
+  int64_t run = block_excl_scan<256>(sum, &carry, part);
+#pragma unroll 8
+  for (int i = s0; i < s1; i++) {
+    pp[i].value_offset = run;
+    run += nn_of(i);
   }
   if (threadIdx.x == 0) {
     job.num_values = carry;

@@ -574,6 +574,7 @@ __global__ void __launch_bounds__(256) k_finalize(JobDev* jobs, int n_jobs, Page
   __syncthreads();
   const PageDev* pg = pages + job.page_base;
   int r = INT32_MAX, d = INT32_MAX;
+#pragma unroll 8
   for (int i = threadIdx.x; i < np; i += 256) {
     if (pg[i].read_status != kOK && i < r) r = i;
     if ((pg[i].page_type == 0 || pg[i].page_type == 3) && pg[i].decode_status != kOK && i < d) d = i;
