@@ -297,7 +297,10 @@ typedef struct pqg_assemble_args {
   int32_t reserved;
   uint8_t* validity;         /* out: ceil(num_slots/8) bytes, LSB-first bits     */
   uint8_t* values_spaced;    /* out: num_slots × value_width, nulls zeroed       */
-  int64_t* offsets;          /* out: num_boundaries+1 entries (cap num_slots+1)  */
+  int64_t* offsets;          /* out: num_boundaries+1 entries (cap num_slots+1): */
+                             /* the SLOT index of each boundary, then num_slots  */
+                             /* (a null or empty list still takes its slot; for  */
+                             /* Arrow LIST element offsets: pqg_assemble_list)   */
   int64_t num_valid;         /* out: #valid slots (= notNull total)              */
   int64_t null_count;        /* out: num_slots - num_valid                       */
   int64_t num_boundaries;    /* out: #boundary slots (rows / objects)            */
