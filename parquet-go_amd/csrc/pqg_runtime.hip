@@ -99,6 +99,10 @@ struct DevBuf {
 };
 
 constexpr int kStages = 10;
+#ifndef PQG_WALK_THREADS
+#define PQG_WALK_THREADS 64
+#endif
+constexpr int kWalkLanes = PQG_WALK_THREADS;  // k_hybrid_walk block size (pqg_levels.hip kWalkThreads)
 // stages timed by pqg_last_timings: scan (K1a-e), list, snappy, setup, walk, levels, nn_scan, values, strings,
 // finalize
 constexpr int kMaxAttempts = 6;  // decode + up to 5 arena grows in one pqg_sync
@@ -426,9 +430,9 @@ static int launch_pipeline(pqg_ctx* c) {
   hipLaunchKernelGGL(k_page_levels, dim3(c->num_cus * 24), dim3(64), 0, s, jobs, pages, list, ctr, Q(1), scratch,
                      streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p);
   if (c->timed) hipEventRecord(c->ev[4], s);
-  const unsigned walk_blocks =
-      (unsigned)std::max<int64_t>(1, std::min<int64_t>((c->list_cap + 255) / 256, c->num_cus * 8));
-  hipLaunchKernelGGL(k_hybrid_walk, dim3(walk_blocks), dim3(256), 0, s, pages, list, ctr, streams, runs, blks);
+  const unsigned walk_blocks = (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>((c->list_cap + kWalkLanes - 1) / kWalkLanes, c->num_cus * (2048 / kWalkLanes)));
+  hipLaunchKernelGGL(k_hybrid_walk, dim3(walk_blocks), dim3(kWalkLanes), 0, s, pages, list, ctr, streams, runs, blks);
   if (c->timed) hipEventRecord(c->ev[5], s);
   if (c->timed) hipEventRecord(c->ev[6], s);
   hipLaunchKernelGGL(k_nn_scan, dim3(n), dim3(256), 0, s, jobs, pages, scratch);
