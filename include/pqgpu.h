@@ -158,6 +158,10 @@ typedef struct pqg_chunk_result {
   int32_t error_page;  /* index into the page list of the failing page, -1 if none */
   int32_t num_pages;   /* pages seen (dictionary page included)                    */
   int32_t value_width; /* bytes per value; 0 = variable length (offsets)           */
+  int32_t col_flags;   /* the job's pqg_column_desc.flags, echoed: bit0 unsigned   */
+                       /* (the Go adapter boxes uint32/uint64 from it, as          */
+                       /* int32PlainDecoder.unSigned does, type_int32.go:29-33)    */
+  int32_t reserved;
   int64_t num_slots;   /* Σ data-page num_values  (= level entries)                */
   int64_t num_values;  /* Σ notNull                                                */
   int64_t values_bytes;

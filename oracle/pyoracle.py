@@ -83,8 +83,9 @@ class OracleChunk:
     """Host-side decoded chunk from the oracle (numpy copies)."""
 
     def __init__(self, status, error_page, pages, num_slots, num_values, def_levels, rep_levels,
-                 values, offsets, value_width):
+                 values, offsets, value_width, col_flags=0):
         self.status = status
+        self.col_flags = col_flags
         self.error_page = error_page
         self.pages = pages
         self.num_slots = num_slots
@@ -115,7 +116,7 @@ def decode_chunk(job: abi.ChunkJob, page_cap: int = 1 << 20) -> OracleChunk:
                       grab(res.def_levels, res.num_slots), grab(res.rep_levels, res.num_slots),
                       grab(res.values, res.values_bytes),
                       grab(res.offsets, (res.num_values + 1) * 8, np.int64) if res.offsets else None,
-                      res.value_width)
+                      res.value_width, res.col_flags)
     L.pqo_free_result(C.byref(res))
     return out
 

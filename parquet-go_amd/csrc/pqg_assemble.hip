@@ -249,7 +249,9 @@ __global__ void __launch_bounds__(1024) k_list_scan(int64_t* seg_cnt, int64_t ns
   }
   if (t == 0) {
     for (int j = 0; j < 4; j++) tot[j] = carry[j];
-    if (list_offsets) list_offsets[carry[0]] = (int32_t)carry[1];
+    // more elements than int32 offsets hold: the host reports PQG_ERR_INVALID_ARG
+    // before any output is written (pqg_assemble_list)
+    if (list_offsets && carry[1] <= INT32_MAX) list_offsets[carry[0]] = (int32_t)carry[1];
   }
 }
 
@@ -317,7 +319,22 @@ __global__ void __launch_bounds__(256) k_list_write(const uint8_t* def_, const u
   }
 }
 
-int list_launch(hipStream_t s, const pqg_list_args* a, int64_t* seg_scratch, int64_t* tot) {
+// Count + scan of the list export; tot[0..3] = rows, elements, valid elements,
+// null lists.  Writes no output but list_offsets[rows] (and that only when the
+// element count fits int32).
+int list_count_launch(hipStream_t s, const pqg_list_args* a, int64_t* seg_scratch, int64_t* tot) {
+  const int64_t n = a->num_slots;
+  const int64_t nseg = (n + kAsmSeg - 1) / kAsmSeg;
+  const unsigned blocks = (unsigned)((nseg + 3) / 4);
+  if (nseg > 0)
+    hipLaunchKernelGGL(k_list_count, dim3(blocks), dim3(256), 0, s, a->def_levels, a->rep_levels, n, a->max_def,
+                       a->list_def, a->elem_def, nseg, seg_scratch);
+  hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(1024), 0, s, seg_scratch, nseg, tot, a->list_offsets);
+  return hipGetLastError() == hipSuccess ? PQG_OK : PQG_ERR_HIP;
+}
+
+// The outputs, after list_count_launch's totals were checked by the host.
+int list_write_launch(hipStream_t s, const pqg_list_args* a, int64_t* seg_scratch) {
   const int64_t n = a->num_slots;
   const int64_t nseg = (n + kAsmSeg - 1) / kAsmSeg;
   const unsigned blocks = (unsigned)((nseg + 3) / 4);
@@ -325,10 +342,6 @@ int list_launch(hipStream_t s, const pqg_list_args* a, int64_t* seg_scratch, int
   const size_t bm_bytes = (size_t)((n + 31) / 32) * 4;  // whole dwords (see pqgpu.h)
   if (a->list_validity && bm_bytes) hipMemsetAsync(a->list_validity, 0, bm_bytes, s);
   if (a->elem_validity && bm_bytes) hipMemsetAsync(a->elem_validity, 0, bm_bytes, s);
-  if (nseg > 0)
-    hipLaunchKernelGGL(k_list_count, dim3(blocks), dim3(256), 0, s, a->def_levels, a->rep_levels, n, a->max_def,
-                       a->list_def, a->elem_def, nseg, seg_scratch);
-  hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(1024), 0, s, seg_scratch, nseg, tot, a->list_offsets);
   if (nseg == 0) return hipGetLastError() == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 #define PQG_LST(WW)                                                                                                  \
   hipLaunchKernelGGL(k_list_write<WW>, dim3(blocks), dim3(256), 0, s, a->def_levels, a->rep_levels, a->values, n,   \

@@ -158,6 +158,13 @@ struct JobDev {
   int64_t run_used, blk_used;  // run-table / block-index entries the pages need (k_page_list)
 };
 
+// k_hybrid_walk block size: its LDS layout (pqg_levels.hip) and its launch
+// (pqg_runtime.hip) share this one definition.
+#ifndef PQG_WALK_THREADS
+#define PQG_WALK_THREADS 64
+#endif
+constexpr int kWalkThreads = PQG_WALK_THREADS;
+
 // Work queues: kQShards heads kQStride ints apart (see queue_pull, pqg_device.h).
 constexpr int kQShards = 8;
 constexpr int kQStride = 32;

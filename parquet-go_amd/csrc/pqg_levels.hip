@@ -70,12 +70,8 @@ __device__ __forceinline__ int reg_stream(const JobDev& job, const PageDev& pg, 
 // earlier.  Positions are 32-bit (a page is < 2 GiB: its sizes are thrift
 // i32); the per-run path is kept short because a single wave per SIMD walks
 // it with nothing to hide its latency behind.
-#ifndef PQG_WALK_THREADS
-#define PQG_WALK_THREADS 64
-#endif
 // one lane per stream: small blocks spread the (latency-bound) lanes over
 // every CU instead of one 256-lane block on each of the first few
-constexpr int kWalkThreads = PQG_WALK_THREADS;
 
 struct LaneRing {
   gcu8 base;       // 16-byte aligned address at or below the stream start

@@ -20,7 +20,8 @@
 
 namespace pqg {
 int assemble_launch(hipStream_t s, const pqg_assemble_args* a, int64_t* seg_scratch, int64_t* tot);  // pqg_assemble.hip
-int list_launch(hipStream_t s, const pqg_list_args* a, int64_t* seg_scratch, int64_t* tot);          // pqg_assemble.hip
+int list_count_launch(hipStream_t s, const pqg_list_args* a, int64_t* seg_scratch, int64_t* tot);    // pqg_assemble.hip
+int list_write_launch(hipStream_t s, const pqg_list_args* a, int64_t* seg_scratch);                  // pqg_assemble.hip
 int pack_levels_launch(hipStream_t s, const uint8_t* levels, int64_t n, int bw, uint8_t* packed);     // pqg_assemble.hip
 }
 
@@ -99,10 +100,7 @@ struct DevBuf {
 };
 
 constexpr int kStages = 10;
-#ifndef PQG_WALK_THREADS
-#define PQG_WALK_THREADS 64
-#endif
-constexpr int kWalkLanes = PQG_WALK_THREADS;  // k_hybrid_walk block size (pqg_levels.hip kWalkThreads)
+constexpr int kWalkLanes = kWalkThreads;  // k_hybrid_walk block size (pqg_common.h)
 // stages timed by pqg_last_timings: scan (K1a-e), list, snappy, setup, walk, levels, nn_scan, values, strings,
 // finalize
 constexpr int kMaxAttempts = 6;  // decode + up to 5 arena grows in one pqg_sync
@@ -122,6 +120,11 @@ struct JobKey {
 };
 
 int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+// Grid of a queue-driven kernel: shard s of a queue (items s, s + 8, ...) is
+// pulled only by blocks with blockIdx & 7 == s (queue_pull, pqg_device.h), so
+// every launch needs at least kQShards blocks or a shard's pages are skipped.
+unsigned qgrid(int64_t blocks) { return (unsigned)std::max<int64_t>(blocks, kQShards); }
 
 int value_width_of(const pqg_column_desc& c) {
   switch (c.physical_type) {
@@ -214,7 +217,11 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
           hipSuccess &&
       occ > 0)
     c->snappy_per_cu = occ;
-  c->counters.grow(4096);
+  // counters: ctr[0..1023] + the kQShards-sharded work queues and the per-stage flags
+  if (c->counters.grow(sizeof(int) * (size_t)(1024 + 10 * kQueueInts))) {
+    pqg_ctx_destroy(c);
+    return PQG_ERR_HIP;
+  }
   *out = c;
   return PQG_OK;
 }
@@ -420,14 +427,14 @@ static int launch_pipeline(pqg_ctx* c) {
   bool any_comp = false;
   for (int i = 0; i < n; i++) any_comp |= c->cur[(size_t)i].col.codec != PQG_CODEC_UNCOMPRESSED;
   if (any_comp) {
-    hipLaunchKernelGGL(k_snappy, dim3(snappy_waves), dim3(64), 0, s, jobs, pages, list, ctr, Q(0), scratch);
+    hipLaunchKernelGGL(k_snappy, dim3(qgrid(snappy_waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(0), scratch);
   }
   if (c->timed) hipEventRecord(c->ev[3], s);
   HStream* streams = (HStream*)c->streams.p;
   RunEnt* runs = (RunEnt*)c->runs.p;
   BlockDesc* blks = (BlockDesc*)c->blks.p;
   // setup + def/rep levels, one wave per data page (value streams registered for the walk)
-  hipLaunchKernelGGL(k_page_levels, dim3(c->num_cus * 24), dim3(64), 0, s, jobs, pages, list, ctr, Q(1), scratch,
+  hipLaunchKernelGGL(k_page_levels, dim3(qgrid(c->num_cus * 24)), dim3(64), 0, s, jobs, pages, list, ctr, Q(1), scratch,
                      streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p);
   if (c->timed) hipEventRecord(c->ev[4], s);
   const unsigned walk_blocks = (unsigned)std::max<int64_t>(
@@ -439,23 +446,23 @@ static int launch_pipeline(pqg_ctx* c) {
   if (c->timed) hipEventRecord(c->ev[7], s);
   // every values kernel takes the whole page list and keeps the pages whose
   // vmode (set by k_page_levels) is its own
-  hipLaunchKernelGGL(k_values<1>, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, Q(3),
+  hipLaunchKernelGGL(k_values<1>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(3),
                      (uint8_t*)c->value_arena.p, streams, runs, blks);
   if (c->any_fixed_other) {
-    hipLaunchKernelGGL(k_values<0>, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, Q(2),
+    hipLaunchKernelGGL(k_values<0>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(2),
                        (uint8_t*)c->value_arena.p, streams, runs, blks);
-    hipLaunchKernelGGL(k_values<3>, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, Q(8),
+    hipLaunchKernelGGL(k_values<3>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(8),
                        (uint8_t*)c->value_arena.p, streams, runs, blks);
   }
   if (c->timed) hipEventRecord(c->ev[8], s);
   if (c->any_var) {
     int64_t* offs = (int64_t*)c->offs_arena.p;
     hipLaunchKernelGGL(k_str_dict, dim3(n), dim3(512), 0, s, jobs, pages, (int64_t*)c->doffs_arena.p);
-    hipLaunchKernelGGL(k_str_plain, dim3(c->num_cus * 4), dim3(512), 0, s, jobs, pages, list, ctr, Q(5), offs);
-    hipLaunchKernelGGL(k_str_count, dim3(waves), dim3(64), 0, s, jobs, pages, list, ctr, Q(4), offs, streams, runs,
+    hipLaunchKernelGGL(k_str_plain, dim3(qgrid(c->num_cus * 4)), dim3(512), 0, s, jobs, pages, list, ctr, Q(5), offs);
+    hipLaunchKernelGGL(k_str_count, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(4), offs, streams, runs,
                        blks);
     hipLaunchKernelGGL(k_char_scan, dim3(n), dim3(256), 0, s, jobs, pages, offs);
-    hipLaunchKernelGGL(k_str_copy, dim3(c->num_cus * 4), dim3(512), 0, s, jobs, pages, list, ctr, Q(6),
+    hipLaunchKernelGGL(k_str_copy, dim3(qgrid(c->num_cus * 4)), dim3(512), 0, s, jobs, pages, list, ctr, Q(6),
                        (uint8_t*)c->value_arena.p, offs);
   }
   if (c->timed) hipEventRecord(c->ev[9], s);
@@ -542,6 +549,7 @@ int pqg_sync(pqg_ctx* c, pqg_chunk_result* results, int n_jobs) {
     r.error_page = d.error_page;
     r.num_pages = d.status == PQG_ERR_CAPACITY ? 0 : d.n_out_pages;
     r.value_width = d.value_width;
+    r.col_flags = c->cur[(size_t)i].col.flags;
     r.num_slots = d.num_slots;
     r.num_values = d.num_values;
     r.values_bytes = d.values_bytes;
@@ -583,7 +591,7 @@ int pqg_assemble_list(pqg_ctx* c, pqg_list_args* a) {
   if (c->asm_seg.grow((size_t)(4 * nseg + 4) * sizeof(int64_t))) return PQG_ERR_HIP;
   int64_t* seg = (int64_t*)c->asm_seg.p;
   int64_t* tot = seg + 4 * nseg;
-  int e = pqg::list_launch(c->stream, a, seg, tot);
+  int e = pqg::list_count_launch(c->stream, a, seg, tot);
   if (e) return e;
   int64_t h[4] = {0, 0, 0, 0};
   if (hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
@@ -593,7 +601,11 @@ int pqg_assemble_list(pqg_ctx* c, pqg_list_args* a) {
   a->num_elements = h[1];
   a->num_valid = h[2];
   a->null_lists = h[3];
-  return h[1] > INT32_MAX ? PQG_ERR_INVALID_ARG : PQG_OK;
+  // int32 offsets cannot hold the elements: fail before any output is written
+  if (h[1] > INT32_MAX) return PQG_ERR_INVALID_ARG;
+  e = pqg::list_write_launch(c->stream, a, seg);
+  if (e) return e;
+  return hip_ok(hipStreamSynchronize(c->stream));
 }
 
 int pqg_decode_chunks(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs, pqg_chunk_result* results) {
@@ -656,7 +668,7 @@ int pqg_block_decompress(pqg_ctx* c, int codec, const uint8_t* src, int64_t n, u
   hipSetDevice(c->device);
   // one block = one page of a one-job batch: k_snappy decodes it into scratch
   if (c->blk_src.grow((size_t)n + 64) || c->blk_dst.grow((size_t)v + 64) ||
-      c->blk_meta.grow(sizeof(JobDev) + sizeof(PageDev) + 64 * sizeof(int)))
+      c->blk_meta.grow(sizeof(JobDev) + sizeof(PageDev) + (2 + kQueueInts) * sizeof(int)))
     return PQG_ERR_HIP;
   JobDev jd;
   memset(&jd, 0, sizeof(jd));
@@ -676,14 +688,15 @@ int pqg_block_decompress(pqg_ctx* c, int codec, const uint8_t* src, int64_t n, u
   uint8_t* meta = (uint8_t*)c->blk_meta.p;
   JobDev* djob = (JobDev*)meta;
   PageDev* dpage = (PageDev*)(meta + sizeof(JobDev));
-  int* ints = (int*)(meta + sizeof(JobDev) + sizeof(PageDev));  // [0] list, [1] total, [2..3] queues
-  int hi[4] = {0, 1, 0, 0};
+  int* ints = (int*)(meta + sizeof(JobDev) + sizeof(PageDev));  // [0] list, [1] total, [2..] the sharded queue
+  int hi[2] = {0, 1};
   if (hipMemcpyAsync(c->blk_src.p, src, (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(djob, &jd, sizeof(jd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(dpage, &pd, sizeof(pd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-      hipMemcpyAsync(ints, hi, sizeof(hi), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+      hipMemcpyAsync(ints, hi, sizeof(hi), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemsetAsync(ints + 2, 0, sizeof(int) * kQueueInts, c->stream) != hipSuccess)
     return PQG_ERR_HIP;
-  hipLaunchKernelGGL(k_snappy, dim3(1), dim3(64), 0, c->stream, djob, dpage, ints, ints + 1, ints + 2,
+  hipLaunchKernelGGL(k_snappy, dim3(qgrid(1)), dim3(64), 0, c->stream, djob, dpage, ints, ints + 1, ints + 2,
                      (uint8_t*)c->blk_dst.p);
   if (hipGetLastError() != hipSuccess) return PQG_ERR_HIP;
   if (hipMemcpyAsync(&pd, dpage, sizeof(pd), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||

@@ -85,6 +85,8 @@ class ChunkResult(C.Structure):
         ("error_page", C.c_int32),
         ("num_pages", C.c_int32),
         ("value_width", C.c_int32),
+        ("col_flags", C.c_int32),
+        ("reserved", C.c_int32),
         ("num_slots", C.c_int64),
         ("num_values", C.c_int64),
         ("values_bytes", C.c_int64),

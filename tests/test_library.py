@@ -63,3 +63,20 @@ def test_planner_rejects_bad_footer():
     for bad in (b"", b"PAR1", b"PAR1xxxxPAR1", b"PAR1" + b"\x00" * 8 + b"\xff\xff\xff\x7fPAR1"):
         with pytest.raises(pqgpu.PqgError):
             pqgpu.ParquetFile(bad)
+
+
+UNSIGNED = [("u32", 1, 1), ("u64", 1, 2), ("i32", 0, 1), ("u8", 1, 1), ("i64", 0, 2)]
+
+
+def test_planner_unsigned_flag():
+    """pqg_column_desc.flags bit0 is getInt32ValuesDecoder's / getInt64ValuesDecoder's
+    unSigned (ConvertedType UINT_8/16/32/64 or INTEGER(isSigned=false),
+    chunk_reader.go:99-141), and the oracle echoes it into the result."""
+    from oracle import pyoracle as O
+    data = open(os.path.join(ROOT, "tests", "golden", "unsigned.parquet"), "rb").read()
+    pf = pqgpu.ParquetFile(data)
+    got = [(c.path.decode(), c.desc.flags & 1, c.desc.physical_type) for c in pf.columns]
+    assert got == UNSIGNED
+    for i in range(pf.num_columns):
+        ch = O.decode_chunk(pf.host_job(0, i)[0])
+        assert ch.status == 0 and ch.col_flags == pf.columns[i].desc.flags
