@@ -233,30 +233,44 @@ void snappy_copy(Buf& o, int64_t off, int64_t len) {
     len -= l;
   }
 }
+// Like golang/snappy's Encode (the reference writer's snappyCompressor,
+// compress.go:42-44 -> vendor/github.com/golang/snappy/encode.go:18-41): the
+// input is cut into independent blocks of maxBlockSize = 65536 bytes
+// (snappy.go:72), each encoded with a fresh match table, so no copy reaches
+// into an earlier block.  g_snappy_block = 0 encodes the page as one block
+// (copies up to 65535 bytes back across any 64 KiB boundary: still a valid
+// stream, which the decoder must handle without the block structure).
+static int64_t g_snappy_block = 65536;
 Buf snappy_compress(const uint8_t* src, int64_t n) {
   Buf o;
   put_uvarint(o, (uint64_t)n);
   const int HB = 14;
   std::vector<int64_t> table((size_t)1 << HB, -1);
-  int64_t i = 0, lit = 0;
-  while (i + 4 <= n) {
-    uint32_t x;
-    memcpy(&x, src + i, 4);
-    uint32_t h = (x * 0x1e35a7bdU) >> (32 - HB);
-    int64_t cand = table[h];
-    table[h] = i;
-    if (cand >= 0 && i - cand <= 65535 && memcmp(src + cand, src + i, 4) == 0) {
-      int64_t len = 4;
-      while (i + len < n && src[cand + len] == src[i + len]) len++;
-      snappy_literal(o, src + lit, i - lit);
-      snappy_copy(o, i - cand, len);
-      i += len;
-      lit = i;
-    } else {
-      i++;
+  const int64_t bs = g_snappy_block > 0 ? g_snappy_block : (n > 0 ? n : 1);
+  for (int64_t b0 = 0; b0 < n || (n == 0 && b0 == 0); b0 += bs) {
+    if (n == 0) break;
+    const int64_t b1 = b0 + bs < n ? b0 + bs : n;
+    std::fill(table.begin(), table.end(), (int64_t)-1);
+    int64_t i = b0, lit = b0;
+    while (i + 4 <= b1) {
+      uint32_t x;
+      memcpy(&x, src + i, 4);
+      uint32_t h = (x * 0x1e35a7bdU) >> (32 - HB);
+      int64_t cand = table[h];
+      table[h] = i;
+      if (cand >= 0 && i - cand <= 65535 && memcmp(src + cand, src + i, 4) == 0) {
+        int64_t len = 4;
+        while (i + len < b1 && src[cand + len] == src[i + len]) len++;
+        snappy_literal(o, src + lit, i - lit);
+        snappy_copy(o, i - cand, len);
+        i += len;
+        lit = i;
+      } else {
+        i++;
+      }
     }
+    snappy_literal(o, src + lit, b1 - lit);
   }
-  snappy_literal(o, src + lit, n - lit);
   return o;
 }
 
@@ -707,6 +721,8 @@ int64_t pqw_dbp_encode32(const int32_t* v, int64_t n, uint8_t* out, int64_t cap)
   memcpy(out, b.data(), b.size());
   return (int64_t)b.size();
 }
+// 65536 (default): golang/snappy's independent 64 KiB blocks; 0: one block
+void pqw_set_snappy_block(int64_t bs) { g_snappy_block = bs; }
 int64_t pqw_snappy_compress(const uint8_t* src, int64_t n, uint8_t* out, int64_t cap) {
   Buf b = snappy_compress(src, n);
   if ((int64_t)b.size() > cap) return -(int64_t)b.size();

@@ -51,6 +51,8 @@ def lib():
         L.pqw_dbp_encode32.restype = C.c_int64
         L.pqw_snappy_compress.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
         L.pqw_snappy_compress.restype = C.c_int64
+        L.pqw_set_snappy_block.argtypes = [C.c_int64]
+        L.pqw_set_snappy_block.restype = None
         _lib = L
     return _lib
 
@@ -139,6 +141,22 @@ def dbp_encode(values, bits=64):
     n = fn(v.ctypes.data, len(v), out.ctypes.data, cap)
     assert n >= 0
     return out[:n].tobytes()
+
+
+class snappy_block_size:
+    """Inside `with snappy_block_size(0):` the writer compresses every snappy page
+    as one block (copies across 64 KiB boundaries) instead of golang/snappy's
+    independent 64 KiB blocks (the default, encode.go:18-41)."""
+
+    def __init__(self, bs):
+        self.bs = bs
+
+    def __enter__(self):
+        lib().pqw_set_snappy_block(self.bs)
+        return self
+
+    def __exit__(self, *a):
+        lib().pqw_set_snappy_block(65536)
 
 
 def snappy_compress(data: bytes):

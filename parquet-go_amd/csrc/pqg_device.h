@@ -44,6 +44,14 @@ __device__ __forceinline__ void sts16(PQG_L void* a, uint4 x) {
   *(PQG_L u32x4_t*)a = v;
 }
 
+// Agent-scope relaxed load: `global_load_dword … sc1`, served by L2 and never
+// by this CU's L1 (MI355X_MICROARCH.md, fence table).  Reading bytes this wave
+// stored earlier needs only its own `s_waitcnt vmcnt(0)` before it — no
+// acquire fence, which would invalidate the whole CU's L1 (≈1.7 µs).
+__device__ __forceinline__ uint32_t ld_l2_u32(const PQG_G uint32_t* p) {
+  return __hip_atomic_load((PQG_G uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr int kWave = 64;
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }

@@ -312,10 +312,12 @@ struct SnapBlock {
       // flush stores have landed and this CU's L1 holds no stale line
       // (off > kRing - 16 > len: no overlap)
       flush(d & ~(int64_t)15);
-      __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __builtin_amdgcn_s_waitcnt(0);  // this wave's flush stores have reached L2
       uint8_t b = 0;
-      if (lane < len) b = dst[h];
+      if (lane < len) {
+        const uintptr_t a = (uintptr_t)(dst + h);
+        b = (uint8_t)(ld_l2_u32((const PQG_G uint32_t*)(a & ~(uintptr_t)3)) >> ((a & 3) * 8));
+      }
       if (lane < len) lds_ptr(sh->ring)[(uint32_t)(d + lane) & (kRing - 1)] = b;
     }
     d += len;
@@ -610,17 +612,16 @@ struct SnapBlock {
       }
       if (__ballot(far)) {
         PQG_SA(14, 1);
-        // flushed output, read through L2: wait for the flush stores, then
-        // invalidate this CU's L1 (a line loaded earlier may hold bytes that
-        // were stored after it was cached)
+        // flushed output, read from L2 (sc1 loads bypass this CU's L1, whose
+        // lines may predate later stores): only this wave's flush stores need
+        // to have landed
         __builtin_amdgcn_s_waitcnt(0);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         uint32_t fw[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) {
           const int64_t h = a0 + own[k];
           const bool f = own[k] < kSpan && h < ring_lo;
-          fw[k] = *(const PQG_G uint32_t*)((uintptr_t)(dst + (f ? h : 0)) & ~(uintptr_t)3);
+          fw[k] = f ? ld_l2_u32((const PQG_G uint32_t*)((uintptr_t)(dst + h) & ~(uintptr_t)3)) : 0u;
         }
 #pragma unroll
         for (int k = 0; k < 16; k++) {
