@@ -143,6 +143,9 @@ def dbp_encode(values, bits=64):
     return out[:n].tobytes()
 
 
+SNAPPY_BLOCK = 65536  # golang/snappy maxBlockSize (snappy.go:72)
+
+
 class snappy_block_size:
     """Inside `with snappy_block_size(0):` the writer compresses every snappy page
     as one block (copies across 64 KiB boundaries) instead of golang/snappy's

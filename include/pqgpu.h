@@ -98,8 +98,12 @@ enum {
 
 /* page_info.flags */
 enum {
-  PQG_PAGE_FLAG_INT96_NIL = 1   /* Q8: truncated final INT96 value left nil by the
+  PQG_PAGE_FLAG_INT96_NIL = 1,  /* Q8: truncated final INT96 value left nil by the
                                    reference (type_int96.go:21-42); bytes are 0 */
+  PQG_PAGE_FLAG_SNAPPY_SERIAL = 2 /* libpqgpu diagnostic: the page's snappy block was
+                                   decoded whole by one wave (its 64 KiB sub-block
+                                   split failed: a copy across a 64 KiB block
+                                   boundary, or a corrupt block) */
 };
 
 /* ---- column / chunk description ----------------------------------------- */

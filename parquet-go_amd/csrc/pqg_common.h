@@ -75,6 +75,23 @@ struct PageDev {
   // and their offset in the chunk's chars (exclusive scan over the pages)
   int64_t chars;
   int64_t char_offset;
+  // K2 snappy split (pqg_snappy.hip, k_snap_plan): bytes of the block's
+  // length varint, 64 KiB output sub-blocks and their SnapSub entries, 4 KiB
+  // compressed segments, and the serial-fallback flag (non-zero: k_snappy
+  // decodes the page as one block)
+  int32_t sn_hdr, sn_nsub, sn_sub_base, sn_nseg, sn_seg_base, sn_fallback;
+};
+
+// K2 snappy sub-block: the output [j * kSnapSub, (j + 1) * kSnapSub) of one
+// compressed block, decoded by one wave from a chain tag at or before its
+// start (found by k_snap_link from the segment exits of k_snap_seg).
+constexpr int kSnapSub = 65536;   // golang/snappy maxBlockSize (snappy.go:72)
+constexpr int kSnapSeg = 4096;    // compressed bytes per segment of the tag-chain search
+struct SnapSub {
+  int32_t page;  // PageDev index
+  int32_t j;     // sub-block of the page
+  int32_t pos;   // block offset of a chain tag whose output starts at `out` (-1: not found)
+  int32_t out;   // output offset of that tag (<= j * kSnapSub)
 };
 
 // One RLE/bit-packed hybrid stream (hybrid_decoder.go): a page's rep or def
@@ -173,6 +190,9 @@ constexpr int kQueueInts = kQShards * kQStride;
 // stage (PageDev.vmode 0..3), set by k_page_levels when a page of that stage
 // exists, so an empty stage's kernel exits at once instead of walking the list
 constexpr int kModePresentOff = 1024 + 9 * kQueueInts;
+// the serial snappy pass (k_snappy after the split decode) pulls its own queue
+constexpr int kQueueSnapSerial = 10;
+constexpr int kQueueSlots = 11;  // queue regions zeroed per launch: 0-8, the stage flags (9), 10
 
 // Scan tiles of the speculative page-header search.
 constexpr int kScanTile = 16384;

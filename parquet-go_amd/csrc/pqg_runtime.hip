@@ -43,6 +43,14 @@ __global__ void k_page_list(JobDev* jobs, PageDev* pages, int n_jobs, int* list,
                             int* queues);
 __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                          uint8_t* scratch);
+__global__ void k_snap_plan(const JobDev* jobs, PageDev* pages, const int* list, const int* total, int* ctr,
+                            SnapSub* subs, int sub_cap, int* seg_page, int seg_cap);
+__global__ void k_snap_seg(const JobDev* jobs, const PageDev* pages, const int* seg_page, const int* seg_total,
+                           int seg_cap, uint2* F);
+__global__ void k_snap_link(const JobDev* jobs, PageDev* pages, const int* list, const int* total, SnapSub* subs,
+                            const uint2* F);
+__global__ void k_snap_decode(const JobDev* jobs, PageDev* pages, const SnapSub* subs, const int* sub_total,
+                              int sub_cap, int* queue, uint8_t* scratch);
 __global__ void k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                               uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena);
 __global__ void k_hybrid_walk(const PageDev* pages, const int* list, const int* total, HStream* streams,
@@ -152,7 +160,9 @@ struct pqg_ctx {
   DevBuf asm_seg;  // K8 per-segment counts + totals
   DevBuf offs_arena, doffs_arena;  // K7: value offsets (int64), dictionary record starts
   DevBuf page_stage;               // pqg_decode_page: [dictionary page][data page]
-  DevBuf blk_src, blk_dst, blk_meta;  // pqg_block_decompress
+  DevBuf blk_src, blk_dst, blk_meta, blk_subs, blk_segpage, blk_F;  // pqg_block_decompress
+  DevBuf sn_subs, sn_segpage, sn_F;   // K2 split: sub-block table, segment -> page, segment exits
+  int64_t sn_sub_cap = 0, sn_seg_cap = 0;
   int64_t total_tiles = 0;
   JobDev* h_jobs = nullptr;  // pinned
   int h_jobs_cap = 0;
@@ -218,7 +228,7 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
       occ > 0)
     c->snappy_per_cu = occ;
   // counters: ctr[0..1023] + the kQShards-sharded work queues and the per-stage flags
-  if (c->counters.grow(sizeof(int) * (size_t)(1024 + 10 * kQueueInts))) {
+  if (c->counters.grow(sizeof(int) * (size_t)(1024 + kQueueSlots * kQueueInts))) {
     pqg_ctx_destroy(c);
     return PQG_ERR_HIP;
   }
@@ -234,7 +244,8 @@ void pqg_ctx_destroy(pqg_ctx* c) {
   for (DevBuf* b : {&c->jobs, &c->pages, &c->list, &c->counters, &c->def_arena, &c->rep_arena, &c->value_arena,
                     &c->scratch, &c->streams, &c->runs, &c->blks, &c->cand_list, &c->vlists, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
                     &c->ok2slot, &c->order, &c->asm_seg, &c->offs_arena, &c->doffs_arena, &c->page_stage,
-                    &c->blk_src, &c->blk_dst, &c->blk_meta, &c->tile_job})
+                    &c->blk_src, &c->blk_dst, &c->blk_meta, &c->tile_job, &c->sn_subs, &c->sn_segpage, &c->sn_F,
+                    &c->blk_subs, &c->blk_segpage, &c->blk_F})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
   hipStreamDestroy(c->stream);
@@ -275,7 +286,7 @@ static int plan_batch(pqg_ctx* c) {
     if (hipHostMalloc((void**)&c->h_jobs, sizeof(JobDev) * (size_t)c->h_jobs_cap) != hipSuccess) return PQG_ERR_HIP;
   }
   int64_t page_total = 0, slot_total = 0, value_total = 0, scratch_total = 0, tile_total = 0, run_total = 0,
-          blk_total = 0, offs_total = 0, doffs_total = 0;
+          blk_total = 0, offs_total = 0, doffs_total = 0, seg_total = 0;
   c->plan.resize((size_t)n);
   for (int i = 0; i < n; i++) {
     const pqg_chunk_job& in = c->cur[(size_t)i];
@@ -319,6 +330,7 @@ static int plan_batch(pqg_ctx* c) {
     d.scratch_cap = xcap;
     d.scratch_base = scratch_total;
     scratch_total += align_up(xcap, 256);
+    if (in.col.codec != PQG_CODEC_UNCOMPRESSED) seg_total += in.total_compressed_size / kSnapSeg + pcap;
     d.dict_page = -1;
     d.error_page = -1;
     const int64_t lim = std::max<int64_t>(0, std::min(in.total_compressed_size, in.data_len));
@@ -352,6 +364,13 @@ static int plan_batch(pqg_ctx* c) {
     c->h_jobs[i] = d;
   }
   c->list_cap = page_total;
+  // K2 split tables: a page of u bytes has ceil(u / 64 KiB) sub-blocks (>= 1)
+  // and a block of b bytes ceil(b / 4 KiB) segments
+  c->sn_sub_cap = scratch_total / kSnapSub + page_total + 64;
+  c->sn_seg_cap = seg_total + 64;
+  if (c->sn_subs.grow(sizeof(SnapSub) * (size_t)c->sn_sub_cap) || c->sn_segpage.grow(sizeof(int) * (size_t)c->sn_seg_cap) ||
+      c->sn_F.grow(sizeof(uint2) * 64 * (size_t)c->sn_seg_cap))
+    return PQG_ERR_HIP;
   if (c->jobs.grow(sizeof(JobDev) * (size_t)n) || c->pages.grow(sizeof(PageDev) * (size_t)page_total) ||
       c->list.grow(sizeof(int) * (size_t)std::max<int64_t>(page_total, 1)) || c->def_arena.grow((size_t)slot_total + 64) ||
       c->rep_arena.grow((size_t)slot_total + 64) || c->value_arena.grow((size_t)value_total + 64) ||
@@ -375,6 +394,31 @@ static int plan_batch(pqg_ctx* c) {
   return hip_ok(hipMemcpyAsync(c->jobs.p, c->h_jobs, sizeof(JobDev) * (size_t)n, hipMemcpyHostToDevice, c->stream));
 }
 
+// K2: the split snappy decode of every compressed page in `list` (pqg_snappy.hip):
+// plan -> segment exits -> chain link -> 64 KiB sub-blocks, then the serial
+// path for the pages it sent back.  sctr: 2 ints (sub-block / segment totals),
+// q_split and q_serial: zeroed sharded queues.
+struct SnapTables {
+  SnapSub* subs;
+  int sub_cap;
+  int* segpage;
+  int seg_cap;
+  uint2* F;
+};
+static void launch_snappy(pqg_ctx* c, hipStream_t s, JobDev* jobs, PageDev* pages, const int* list, const int* total,
+                          int64_t list_cap, int* sctr, int* q_split, int* q_serial, uint8_t* scratch,
+                          const SnapTables& T) {
+  const int waves = c->num_cus * c->snappy_per_cu;  // as many as fit (LDS: the history ring)
+  hipMemsetAsync(sctr, 0, 2 * sizeof(int), s);
+  hipLaunchKernelGGL(k_snap_plan, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((list_cap + 255) / 256, c->num_cus * 4))),
+                     dim3(256), 0, s, jobs, pages, list, total, sctr, T.subs, T.sub_cap, T.segpage, T.seg_cap);
+  hipLaunchKernelGGL(k_snap_seg, dim3(c->num_cus * 16), dim3(64), 0, s, jobs, pages, T.segpage, sctr + 1, T.seg_cap, T.F);
+  hipLaunchKernelGGL(k_snap_link, dim3(c->num_cus * 4), dim3(64), 0, s, jobs, pages, list, total, T.subs, T.F);
+  hipLaunchKernelGGL(k_snap_decode, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, T.subs, sctr, T.sub_cap, q_split,
+                     scratch);
+  hipLaunchKernelGGL(k_snappy, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, total, q_serial, scratch);
+}
+
 static int launch_pipeline(pqg_ctx* c) {
   const int n = c->n_jobs;
   c->launches++;
@@ -391,10 +435,9 @@ static int launch_pipeline(pqg_ctx* c) {
   // page-queue kernels: one wave per page; enough waves per SIMD to hide the
   // dependent HBM reads (bounded by VGPRs / LDS per kernel)
   const int waves = c->num_cus * 20;
-  const int snappy_waves = c->num_cus * c->snappy_per_cu;  // as many as fit (LDS: the history ring)
   hipStream_t s = c->stream;
   if (c->timed) hipEventRecord(c->ev[0], s);
-  hipMemsetAsync(Q(0), 0, sizeof(int) * 10 * kQueueInts, s);  // queues + the stage flags (kModePresentOff)
+  hipMemsetAsync(Q(0), 0, sizeof(int) * kQueueSlots * kQueueInts, s);  // queues + the stage flags (kModePresentOff)
   const int64_t nt = c->total_tiles;
   int* tcount = (int*)c->tile_count.p;
   int* toff = (int*)c->tile_off.p;
@@ -427,7 +470,9 @@ static int launch_pipeline(pqg_ctx* c) {
   bool any_comp = false;
   for (int i = 0; i < n; i++) any_comp |= c->cur[(size_t)i].col.codec != PQG_CODEC_UNCOMPRESSED;
   if (any_comp) {
-    hipLaunchKernelGGL(k_snappy, dim3(qgrid(snappy_waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(0), scratch);
+    const SnapTables T{(SnapSub*)c->sn_subs.p, (int)std::min<int64_t>(c->sn_sub_cap, INT32_MAX), (int*)c->sn_segpage.p,
+                       (int)std::min<int64_t>(c->sn_seg_cap, INT32_MAX), (uint2*)c->sn_F.p};
+    launch_snappy(c, s, jobs, pages, list, ctr, c->list_cap, ctr + 32, Q(0), Q(kQueueSnapSerial), scratch, T);
   }
   if (c->timed) hipEventRecord(c->ev[3], s);
   HStream* streams = (HStream*)c->streams.p;
@@ -668,7 +713,11 @@ int pqg_block_decompress(pqg_ctx* c, int codec, const uint8_t* src, int64_t n, u
   hipSetDevice(c->device);
   // one block = one page of a one-job batch: k_snappy decodes it into scratch
   if (c->blk_src.grow((size_t)n + 64) || c->blk_dst.grow((size_t)v + 64) ||
-      c->blk_meta.grow(sizeof(JobDev) + sizeof(PageDev) + (2 + kQueueInts) * sizeof(int)))
+      c->blk_meta.grow(sizeof(JobDev) + sizeof(PageDev) + (4 + 2 * kQueueInts) * sizeof(int)))
+    return PQG_ERR_HIP;
+  const int64_t bsub = (int64_t)v / kSnapSub + 2, bseg = n / kSnapSeg + 2;
+  if (c->blk_subs.grow(sizeof(SnapSub) * (size_t)bsub) || c->blk_segpage.grow(sizeof(int) * (size_t)bseg) ||
+      c->blk_F.grow(sizeof(uint2) * 64 * (size_t)bseg))
     return PQG_ERR_HIP;
   JobDev jd;
   memset(&jd, 0, sizeof(jd));
@@ -688,16 +737,19 @@ int pqg_block_decompress(pqg_ctx* c, int codec, const uint8_t* src, int64_t n, u
   uint8_t* meta = (uint8_t*)c->blk_meta.p;
   JobDev* djob = (JobDev*)meta;
   PageDev* dpage = (PageDev*)(meta + sizeof(JobDev));
-  int* ints = (int*)(meta + sizeof(JobDev) + sizeof(PageDev));  // [0] list, [1] total, [2..] the sharded queue
+  // ints: [0] list, [1] total, [2..3] split counters, then the two sharded queues
+  int* ints = (int*)(meta + sizeof(JobDev) + sizeof(PageDev));
   int hi[2] = {0, 1};
   if (hipMemcpyAsync(c->blk_src.p, src, (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(djob, &jd, sizeof(jd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(dpage, &pd, sizeof(pd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(ints, hi, sizeof(hi), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-      hipMemsetAsync(ints + 2, 0, sizeof(int) * kQueueInts, c->stream) != hipSuccess)
+      hipMemsetAsync(ints + 4, 0, sizeof(int) * 2 * kQueueInts, c->stream) != hipSuccess)
     return PQG_ERR_HIP;
-  hipLaunchKernelGGL(k_snappy, dim3(qgrid(1)), dim3(64), 0, c->stream, djob, dpage, ints, ints + 1, ints + 2,
-                     (uint8_t*)c->blk_dst.p);
+  // the page decode's own snappy stage, on a one-page list
+  const SnapTables T{(SnapSub*)c->blk_subs.p, (int)bsub, (int*)c->blk_segpage.p, (int)bseg, (uint2*)c->blk_F.p};
+  launch_snappy(c, c->stream, djob, dpage, ints, ints + 1, 1, ints + 2, ints + 4, ints + 4 + kQueueInts,
+                (uint8_t*)c->blk_dst.p, T);
   if (hipGetLastError() != hipSuccess) return PQG_ERR_HIP;
   if (hipMemcpyAsync(&pd, dpage, sizeof(pd), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
@@ -752,7 +804,8 @@ int pqg_get_pages(pqg_ctx* c, int job, pqg_page_info* out, int cap) {
     o.def_encoding = p.def_enc;
     o.rep_encoding = p.rep_enc;
     o.status = p.read_status != PQG_OK ? p.read_status : p.decode_status;
-    o.flags = p.flags;
+    // bits 8+: why the split snappy decode gave the page up (diagnostics, pqg_snappy.hip)
+    o.flags = p.flags | (p.sn_fallback ? PQG_PAGE_FLAG_SNAPPY_SERIAL | (p.sn_fallback << 8) : 0);
   }
   return k;
 }

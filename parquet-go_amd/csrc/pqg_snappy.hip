@@ -112,11 +112,9 @@ struct Tag {
   bool lit, err;
 };
 
-__device__ __forceinline__ Tag parse_tag(const PQG_L uint8_t* in, uint32_t wo, int64_t pos, int64_t slen, int rel) {
-  const PQG_L uint32_t* q = (const PQG_L uint32_t*)(in + (wo & ~3u));
-  const uint32_t a = q[0], b = q[1], c = q[2];
-  const uint32_t sft = (wo & 3) * 8;
-  const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sft), hi = __builtin_amdgcn_alignbit(c, b, sft);
+// lo, hi: the bytes [pos, pos + 8) of the block (decode_other.go:21-80 reads
+// at most 5 of them)
+__device__ __forceinline__ Tag parse_tag_bytes(uint32_t lo, uint32_t hi, int64_t pos, int64_t slen, int rel) {
   const uint32_t tag = lo & 0xff;
   const uint32_t w4 = (lo >> 8) | (hi << 24);  // bytes 1..4
   Tag t;
@@ -151,6 +149,84 @@ __device__ __forceinline__ Tag parse_tag(const PQG_L uint8_t* in, uint32_t wo, i
   return t;
 }
 
+__device__ __forceinline__ Tag parse_tag(const PQG_L uint8_t* in, uint32_t wo, int64_t pos, int64_t slen, int rel) {
+  const PQG_L uint32_t* q = (const PQG_L uint32_t*)(in + (wo & ~3u));
+  const uint32_t a = q[0], b = q[1], c = q[2];
+  const uint32_t sft = (wo & 3) * 8;
+  return parse_tag_bytes(__builtin_amdgcn_alignbit(b, a, sft), __builtin_amdgcn_alignbit(c, b, sft), pos, slen, rel);
+}
+
+// bytes [p, p + 8) of a block in global memory; dwords holding no byte of
+// [0, slen) read as 0 (a dword holding one is mapped)
+__device__ __forceinline__ void ld8_block(gcu8 src, int64_t slen, int64_t p, uint32_t& lo, uint32_t& hi) {
+  const uintptr_t a = (uintptr_t)(src + p), q = a & ~(uintptr_t)3, end = (uintptr_t)(src + slen);
+  const uint32_t w0 = q < end ? *(const PQG_G uint32_t*)q : 0u;
+  const uint32_t w1 = q + 4 < end ? *(const PQG_G uint32_t*)(q + 4) : 0u;
+  const uint32_t w2 = q + 8 < end ? *(const PQG_G uint32_t*)(q + 8) : 0u;
+  const uint32_t sft = (uint32_t)(a & 3) * 8;
+  lo = __builtin_amdgcn_alignbit(w1, w0, sft);
+  hi = __builtin_amdgcn_alignbit(w2, w1, sft);
+}
+
+__device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) {  // a, b <= 2^31 - 1
+  const uint32_t c = a + b;
+  return c > 0x7fffffffu ? 0x7fffffffu : c;
+}
+__device__ __forceinline__ uint32_t bperm(uint32_t v, int from_lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(from_lane << 2, (int)v);
+}
+
+// ---------------------------------------------------------------------------
+// Tag-chain walk by pointer doubling (the split of big blocks, see k_snap_seg).
+// Every lane follows its own chain position x (a block offset) to the first
+// chain position >= hi, adding the output bytes of the tags it passes to acc.
+// Each step takes the 64 positions from the smallest x still below hi: every
+// lane parses the tag at one of them (speculatively), and six ds_bpermute
+// doubling rounds give each position its exit from those 64 (or the first
+// position >= hi inside them, which points at itself) and the output bytes on
+// the way, so every chain in the window advances past it at once.
+// ---------------------------------------------------------------------------
+__device__ void chain_walk(gcu8 src, int64_t slen, int64_t hi, int64_t& x, uint32_t& acc) {
+  const int lane = lane_id();
+  for (;;) {
+    const bool act = x < hi;
+    if (!__ballot(act)) break;
+    uint32_t xm = act ? (uint32_t)x : 0xffffffffu;  // block offsets are < 2^31
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint32_t y = (uint32_t)__shfl_xor((int)xm, o, 64);
+      xm = y < xm ? y : xm;
+    }
+    const int64_t wb = (int64_t)__builtin_amdgcn_readfirstlane(xm);
+    const int64_t p = wb + lane;
+    uint32_t lo, hw;
+    ld8_block(src, slen, p, lo, hw);
+    const Tag t = parse_tag_bytes(lo, hw, p, slen, lane);
+    uint32_t J = t.next < 0x7fffffff ? (uint32_t)t.next : 0x7fffffffu;  // relative to wb
+    uint32_t O = t.len < (1 << 30) ? (uint32_t)t.len : (1u << 30);
+    if (p >= hi) {  // the walk ends at the first chain position >= hi: a fixed point
+      J = (uint32_t)lane;
+      O = 0;
+    }
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+      const bool in = J < 64;
+      const uint32_t Jn = bperm(J, in ? (int)J : lane), On = bperm(O, in ? (int)J : lane);
+      if (in) {
+        J = Jn;
+        O = sat_add(O, On);
+      }
+    }
+    const int64_t rel = x - wb;
+    const bool here = act && rel < 64;
+    const uint32_t Jx = bperm(J, here ? (int)rel : lane), Ox = bperm(O, here ? (int)rel : lane);
+    if (here) {
+      x = wb + (int64_t)Jx;
+      acc = sat_add(acc, Ox);
+    }
+  }
+}
+
 struct SnapBlock {
   gcu8 src;
   int64_t slen;
@@ -160,6 +236,12 @@ struct SnapBlock {
   int64_t d = 0;        // output bytes produced
   int64_t flushed = 0;  // output bytes stored (16-aligned until the end)
   int64_t in_base = kFarAway;
+  // A sub-block decode (k_snap_decode) produces the output [base, dend) only
+  // and may read no output before base; the whole block is base 0, dend dlen.
+  // Any tag that cannot be decoded that way (corrupt, or a copy reaching
+  // before base) fails the decode, and the page is decoded serially.
+  int64_t base = 0;
+  int64_t dend = -1;
 #ifdef PQG_PROFILE
   uint64_t pacc[16] = {0};
 #define PQG_ST(v) const uint64_t v = __builtin_amdgcn_s_memtime()
@@ -340,7 +422,8 @@ struct SnapBlock {
   __device__ int serial(int64_t& s, int max) {
     int short_streak = 0;
     uint64_t x8 = peek8(s);
-    for (int n = 0; n < max && s < slen && short_streak < 4; n++) {
+    const bool lastsub = dend == dlen;
+    for (int n = 0; n < max && s < slen && short_streak < 4 && (lastsub || d < dend); n++) {
       const uint32_t tag = (uint32_t)x8 & 0xff;
       int64_t length, ns;
       uint32_t offset = 0;
@@ -356,7 +439,7 @@ struct SnapBlock {
           x = (uint32_t)(x8 >> 8) & (nb == 4 ? 0xffffffffu : ((1u << (8 * nb)) - 1));
         }
         length = (int64_t)x + 1;
-        if (length > dlen - d || length > slen - (s + hdr)) return kSNAPPY;
+        if (length > dend - d || length > slen - (s + hdr)) return kSNAPPY;
         ns = s + hdr + length;
       } else {
         hdr = (tag & 3) == 1 ? 2 : (tag & 3) == 2 ? 3 : 5;
@@ -371,7 +454,7 @@ struct SnapBlock {
           length = 1 + (tag >> 2);
           offset = (uint32_t)(x8 >> 8);
         }
-        if (offset == 0 || (int64_t)offset > d || length > dlen - d) return kSNAPPY;
+        if (offset == 0 || (int64_t)offset > d - base || length > dend - d) return kSNAPPY;
         ns = s + hdr;
       }
       short_streak = length < 16 ? short_streak + 1 : 0;
@@ -402,7 +485,9 @@ struct SnapBlock {
     PQG_ST(t_run0);
     const PQG_L uint8_t* IN = lds_ptr(sh->in);
     int serial_next = 0;  // tags to take one at a time before the next windowed resolution
-    while (s < slen) {
+    if (dend < 0) dend = dlen;
+    const bool lastsub = dend == dlen;  // the block's last sub-block: every tag up to slen is its own
+    while (s < slen && (lastsub || d < dend)) {
       PQG_ST(ta);
       PQG_SA(8, 1);
       if (s < in_base || s + kSnWinNeed > in_base + kSnWin) {
@@ -458,9 +543,10 @@ struct SnapBlock {
       const int pre = (int)(d - a0);
       auto check = [&](const Tag& t, int64_t st, int64_t pos, bool& cut) {
         const int64_t dt = d + st;
-        bool e = t.err || t.len > dlen - dt;                       // length > len(dst)-d
-        if (!t.lit) e |= t.info == 0 || (int64_t)t.info > dt;       // offset <= 0 || d < offset
-        cut = pre + st + t.len > kSpan || (t.lit && pos + t.hdr + t.len > in_base + kSnWin);
+        const bool past = !lastsub && dt >= dend;                       // the next sub-block's tag
+        bool e = !past && (t.err || t.len > dend - dt);                 // length > len(dst)-d
+        if (!t.lit) e |= !past && (t.info == 0 || (int64_t)t.info > dt - base);  // offset <= 0 || d < offset
+        cut = past || pre + st + t.len > kSpan || (t.lit && pos + t.hdr + t.len > in_base + kSnWin);
         return e;
       };
       bool c0, c1;
@@ -645,12 +731,315 @@ struct SnapBlock {
     }
     PQG_ST(t_run1);
     PQG_SA(15, t_run1 - t_run0);
-    if (d != dlen) return kSNAPPY;
-    flush((dlen + 15) & ~(int64_t)15);
+    if (d != dend) return kSNAPPY;
+    flush((dend + 15) & ~(int64_t)15);
     return kOK;
+  }
+
+  // Follow the tag chain from s (output d) to the tag whose output starts at
+  // `target`, without producing output: the start of a sub-block found from a
+  // chain tag before it.  kSNAPPY if a tag straddles target or the chain
+  // leaves the block.
+  __device__ int skip_to(int64_t& s, int64_t target) {
+    const int lane = lane_id();
+    const PQG_L uint8_t* IN = lds_ptr(sh->in);
+    while (d < target) {
+      if (s >= slen) return kSNAPPY;
+      if (s < in_base || s + kSnWinNeed > in_base + kSnWin) fill(s);
+      const uint32_t wo = (uint32_t)(s - in_base) + lane;
+      const Tag t0 = parse_tag(IN, wo, s + lane, slen, lane);
+      const Tag t1 = parse_tag(IN, wo + 64, s + 64 + lane, slen, 64 + lane);
+      const uint32_t n0 = (uint32_t)(t0.next < kPos ? t0.next : kPos), n1 = (uint32_t)(t1.next < kPos ? t1.next : kPos);
+      const uint32_t l0 = (uint32_t)(t0.len < (1 << 30) ? t0.len : (1 << 30)),
+                     l1 = (uint32_t)(t1.len < (1 << 30) ? t1.len : (1 << 30));
+      const int64_t lim64 = slen - s;
+      const int lim = lim64 < kPos ? (int)lim64 : kPos;
+      int p = 0;
+      while (p < lim && d < target) {
+        const bool h = p >= 64;
+        const int l = p & 63;
+        const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)(h ? l1 : l0), l);
+        const bool er = __builtin_amdgcn_readlane((int)(h ? t1.err : t0.err), l) != 0;
+        if (er || d + (int64_t)len > target) return kSNAPPY;
+        d += len;
+        const int np = __builtin_amdgcn_readlane((int)(h ? n1 : n0), l);
+        if (np >= kPos) {  // the tag's bytes run past the parsed positions
+          s += h ? readlane64(t1.next, l) : readlane64(t0.next, l);
+          p = -1;
+          break;
+        }
+        p = np;
+      }
+      if (p >= 0) s += p;
+    }
+    return d == target ? kOK : kSNAPPY;
   }
 };
 
+// The compressed block of a page: V2 pages keep their level bytes raw in
+// front of it (page_v2.go:110-123).
+struct SnapLoc {
+  int64_t src_off, clen, ulen;
+};
+__device__ __forceinline__ SnapLoc snap_loc(const PageDev& pg) {
+  SnapLoc L{pg.payload_offset, pg.csize, pg.usize};
+  if (pg.page_type == 3) {
+    int32_t levels = (int32_t)((uint32_t)pg.rep_len + (uint32_t)pg.def_len);
+    if (levels > 0) L.src_off += levels;
+    L.clen = (int32_t)((uint32_t)pg.csize - (uint32_t)levels);
+    L.ulen = (int32_t)((uint32_t)pg.usize - (uint32_t)levels);
+  }
+  return L;
+}
+
+// decodedLen: binary.Uvarint over the block (decode.go:32-43); kOK, kSNAPPY or
+// kSIZE (a length other than the page's uncompressed size)
+template <class RD>
+__device__ __forceinline__ int snappy_header(RD byte_at, int64_t clen, int64_t ulen, int* hl) {
+  uint64_t v = 0;
+  int e = kOK;
+  unsigned sft = 0;
+  *hl = 0;
+  for (int i = 0;; i++) {
+    if (i >= clen) return kSNAPPY;
+    const int b = byte_at(i);
+    if (b < 0x80) {
+      if (i > 9 || (i == 9 && b > 1)) e = kSNAPPY;
+      else v |= (sft < 64 ? (uint64_t)b << sft : 0);
+      *hl = i + 1;
+      break;
+    }
+    if (sft < 64) v |= (uint64_t)(b & 0x7f) << sft;
+    sft += 7;
+  }
+  if (e == kOK && v > 0xffffffffull) e = kSNAPPY;
+  if (e == kOK && (int64_t)v != ulen) e = kSIZE;
+  return e;
+}
+
+// ============================================================================
+// K2 split: every compressed page is decoded as 64 KiB output sub-blocks, one
+// wave each.  golang/snappy's Encode — the reference writer's snappyCompressor
+// (compress.go:42-44, vendor/github.com/golang/snappy/encode.go:18-41) — and
+// the C++ snappy behind other writers encode independent 64 KiB blocks, so a
+// sub-block's copies stay inside it and its first tag starts exactly at
+// j * 64 KiB of output.  Where a stream does not have that shape (or is
+// corrupt) a sub-block decode fails and the page is decoded serially from the
+// start by k_snappy, which also reports the reference's error.
+//   k_snap_plan   per page: length varint, sub-block and segment table slots
+//   k_snap_seg    per 4 KiB segment of a big block: the chain exit and output
+//                 bytes from each of the segment's first 64 positions
+//   k_snap_link   per big page: chain the segment exits -> a chain tag at or
+//                 before every sub-block start
+//   k_snap_decode per sub-block: skip to its start, decode it (SnapBlock)
+//   k_snappy      pages whose split failed: the whole block on one wave
+// ============================================================================
+__global__ void __launch_bounds__(256) k_snap_plan(const JobDev* jobs, PageDev* pages, const int* list,
+                                                   const int* total, int* ctr, SnapSub* subs, int sub_cap,
+                                                   int* seg_page, int seg_cap) {
+  __shared__ int64_t part[5];
+  __shared__ int s_base[2];
+  const int n = *total;
+  for (int b0 = blockIdx.x * 256; b0 < n; b0 += gridDim.x * 256) {
+    const int t = b0 + (int)threadIdx.x;
+    int nsub = 0, nseg = 0, hdr = 0, fb = 0;
+    int pidx = -1;
+    bool split = false;
+    if (t < n) {
+      pidx = list[t];
+      PageDev& pg = pages[pidx];
+      if (pg.read_status == kOK && pg.scratch_offset >= 0) {
+        const JobDev& job = jobs[pg.job];
+        const SnapLoc L = snap_loc(pg);
+        const PQG_G uint8_t* src = gconst(job.data) + L.src_off;
+        const int e = snappy_header([&](int i) { return (int)src[i]; }, L.clen, L.ulen, &hdr);
+        if (e != kOK) {
+          pg.read_status = e;
+        } else if (pg.page_type == 0 && !values_supported(job.type, job.type_length, pg.encoding)) {
+          fb = 1;  // V1: the values decoder is chosen after decompression (page_v1.go:91-97)
+        } else {
+          split = true;
+          nsub = L.ulen > 0 ? (int)((L.ulen + kSnapSub - 1) / kSnapSub) : 1;
+          nseg = nsub > 1 ? (int)((L.clen - hdr + kSnapSeg - 1) / kSnapSeg) : 0;
+        }
+      }
+    }
+    int64_t tsub, tseg;
+    const int64_t esub = block_excl_scan<256>(nsub, &tsub, part);
+    const int64_t eseg = block_excl_scan<256>(nseg, &tseg, part);
+    if (threadIdx.x == 0) {
+      s_base[0] = tsub ? atomicAdd(ctr, (int)tsub) : 0;
+      s_base[1] = tseg ? atomicAdd(ctr + 1, (int)tseg) : 0;
+    }
+    __syncthreads();
+    if (t < n) {
+      PageDev& pg = pages[pidx];
+      const int64_t sb = s_base[0] + esub, gb = s_base[1] + eseg;
+      if (split && (sb + nsub > sub_cap || gb + nseg > seg_cap)) {
+        split = false;
+        fb = 1;  // tables full: the serial path
+      }
+      if (split) {
+        for (int j = 0; j < nsub; j++) subs[sb + j] = SnapSub{pidx, j, j == 0 ? hdr : -1, 0};
+        for (int k = 0; k < nseg; k++) seg_page[gb + k] = pidx;
+      }
+      pg.sn_hdr = hdr;
+      pg.sn_nsub = split ? nsub : 0;
+      pg.sn_sub_base = (int32_t)sb;
+      pg.sn_nseg = split ? nseg : 0;
+      pg.sn_seg_base = (int32_t)gb;
+      pg.sn_fallback = fb;
+    }
+    __syncthreads();
+  }
+}
+
+// One wave per segment [b, b + 4 KiB) of a big block: from each entry b + lane
+// the chain position where the tag chain leaves the segment, and the output
+// bytes of the tags on the way.  The true chain enters a segment within its
+// first 64 bytes unless a literal longer than that ends inside it.
+__global__ void __launch_bounds__(64) k_snap_seg(const JobDev* jobs, const PageDev* pages, const int* seg_page,
+                                                 const int* seg_total, int seg_cap, uint2* F) {
+  const int lane = lane_id();
+  const int n = min(*seg_total, seg_cap);
+  for (int g = blockIdx.x; g < n; g += gridDim.x) {
+    const int pidx = __builtin_amdgcn_readfirstlane(seg_page[g]);
+    const PageDev pg = pages[pidx];
+    const JobDev job = jobs[pg.job];
+    const SnapLoc L = snap_loc(pg);
+    const int64_t b = pg.sn_hdr + (int64_t)(g - pg.sn_seg_base) * kSnapSeg;
+    const int64_t hi = b + kSnapSeg < L.clen ? b + kSnapSeg : L.clen;
+    int64_t x = b + lane;
+    uint32_t acc = 0;
+    chain_walk(gconst(job.data) + L.src_off, L.clen, hi, x, acc);
+    F[(int64_t)g * 64 + lane] = make_uint2(x < 0x7fffffff ? (uint32_t)x : 0x7fffffffu, acc);
+  }
+}
+
+// One wave per big page: the tag chain from the first tag, hopping a segment
+// at a time through the exits of k_snap_seg (an entry past a segment's first
+// 64 bytes — after a long literal — walks that segment here), recording for
+// each sub-block the last chain tag at or before its first output byte.  A
+// chain that does not end exactly at the block's end with the page's
+// uncompressed size sends the page to the serial path.
+__global__ void __launch_bounds__(64) k_snap_link(const JobDev* jobs, PageDev* pages, const int* list,
+                                                  const int* total, SnapSub* subs, const uint2* F) {
+  const int lane = lane_id();
+  const int n = *total;
+  for (int t = blockIdx.x; t < n; t += gridDim.x) {
+    const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
+    const PageDev pg = pages[pidx];
+    if (pg.read_status != kOK || pg.scratch_offset < 0 || pg.sn_fallback || pg.sn_nsub <= 1) continue;
+    const JobDev job = jobs[pg.job];
+    const SnapLoc L = snap_loc(pg);
+    gcu8 src = gconst(job.data) + L.src_off;
+    const int nseg = pg.sn_nseg, nsub = pg.sn_nsub;
+    const int64_t hdr = pg.sn_hdr;
+    const uint2* Fp = F + (int64_t)pg.sn_seg_base * 64;
+    int64_t e = hdr, o = 0;
+    int j = 1;  // sub-block 0 starts at the first tag (k_snap_plan)
+    int why = 0;  // sn_fallback reason (diagnostics: pqg_page_info.flags >> 8)
+    // rows of 8 segments at a time (lane = entry), the next 8 loaded ahead
+    int kb = 0;
+    uint2 ra[8], rb[8];
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      ra[r] = r < nseg ? Fp[(int64_t)r * 64 + lane] : make_uint2(0, 0);
+      rb[r] = 8 + r < nseg ? Fp[(int64_t)(8 + r) * 64 + lane] : make_uint2(0, 0);
+    }
+    while (e < L.clen) {
+      const int k = (int)((e - hdr) / kSnapSeg);
+      if (k >= nseg) {
+        why = 4;
+        break;
+      }
+      const int64_t b = hdr + (int64_t)k * kSnapSeg;
+      const int rel = (int)(e - b);
+      int64_t x;
+      uint32_t out;
+      if (rel < 64) {
+        if (k >= kb + 16 || k < kb) {  // a jump (long literal): reload both row sets
+          kb = k;
+#pragma unroll
+          for (int r = 0; r < 8; r++) {
+            ra[r] = kb + r < nseg ? Fp[(int64_t)(kb + r) * 64 + lane] : make_uint2(0, 0);
+            rb[r] = kb + 8 + r < nseg ? Fp[(int64_t)(kb + 8 + r) * 64 + lane] : make_uint2(0, 0);
+          }
+        } else if (k >= kb + 8) {  // advance by 8: the prefetched set becomes current
+          kb += 8;
+#pragma unroll
+          for (int r = 0; r < 8; r++) {
+            ra[r] = rb[r];
+            rb[r] = kb + 8 + r < nseg ? Fp[(int64_t)(kb + 8 + r) * 64 + lane] : make_uint2(0, 0);
+          }
+        }
+        uint2 row = ra[0];
+#pragma unroll
+        for (int r = 1; r < 8; r++) row = k - kb == r ? ra[r] : row;
+        x = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)row.x, rel);
+        out = (uint32_t)__builtin_amdgcn_readlane((int)row.y, rel);
+      } else {
+        x = e;
+        out = 0;
+        chain_walk(src, L.clen, b + kSnapSeg < L.clen ? b + kSnapSeg : L.clen, x, out);
+        x = (int64_t)__builtin_amdgcn_readfirstlane((int)x);
+        out = (uint32_t)__builtin_amdgcn_readfirstlane((int)out);
+      }
+      while (j < nsub && (int64_t)j * kSnapSub < o + (int64_t)out) {
+        if (lane == 0) subs[pg.sn_sub_base + j] = SnapSub{pidx, j, (int32_t)e, (int32_t)o};
+        j++;
+      }
+      if (x <= e || out >= 0x7fffffffu) {
+        why = 8;
+        break;
+      }
+      e = x;
+      o += out;
+      if (o > L.ulen) {
+        why = 16;
+        break;
+      }
+    }
+    if (!why && (e != L.clen || o != L.ulen || j != nsub)) why = 32;
+    if (why && lane == 0) pages[pidx].sn_fallback = why;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_snap_decode(const JobDev* jobs, PageDev* pages, const SnapSub* subs,
+                                                    const int* sub_total, int sub_cap, int* queue, uint8_t* scratch) {
+  __shared__ __attribute__((aligned(16))) SnapShared sh;
+  const int lane = lane_id();
+  const int n = min(*sub_total, sub_cap);
+  for (;;) {
+    const int t = queue_next(queue);
+    if (t >= n) return;
+    const SnapSub sb = subs[t];
+    const PageDev pg = pages[sb.page];
+    if (pg.sn_fallback || sb.pos < 0) continue;
+    const JobDev job = jobs[pg.job];
+    const SnapLoc L = snap_loc(pg);
+    SnapBlock blk{gconst(job.data) + L.src_off, L.clen, gmut(scratch) + job.scratch_base + pg.scratch_offset, L.ulen,
+                  &sh};
+    blk.base = (int64_t)sb.j * kSnapSub;
+    blk.dend = blk.base + kSnapSub < L.ulen ? blk.base + kSnapSub : L.ulen;
+    int64_t s = sb.pos;
+    blk.d = sb.out;
+    int e = blk.d < blk.base ? blk.skip_to(s, blk.base) : (blk.d == blk.base ? kOK : kSNAPPY);
+    int why = e != kOK ? 64 : 0;
+    blk.d = blk.flushed = blk.base;
+    if (e == kOK) {
+      e = blk.run(s);
+      if (e != kOK) why = 128;
+    }
+#ifdef PQG_PROFILE
+    for (int k = 0; k < 16; k++) PQG_ACC(k, 0, blk.pacc[k]);
+#endif
+    if (why && lane == 0) atomicOr(&pages[sb.page].sn_fallback, why);
+  }
+}
+
+// The serial path: pages whose split decode failed (k_snap_plan / k_snap_link
+// / k_snap_decode set sn_fallback), decoded from the start on one wave.
 __global__ void __launch_bounds__(64) k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total,
                                                int* queue, uint8_t* scratch) {
   __shared__ __attribute__((aligned(16))) SnapShared sh;
@@ -660,40 +1049,14 @@ __global__ void __launch_bounds__(64) k_snappy(JobDev* jobs, PageDev* pages, con
     if (t >= *total) return;
     const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
     const PageDev pg = pages[pidx];  // locals via scalar loads (see k_levels_expand)
-    if (pg.read_status != kOK || pg.scratch_offset < 0) continue;
-    // compressed block location (V2: after the raw level bytes)
-    int64_t src_off = pg.payload_offset;
-    int64_t clen = pg.csize, ulen = pg.usize;
-    if (pg.page_type == 3) {
-      int32_t levels = (int32_t)((uint32_t)pg.rep_len + (uint32_t)pg.def_len);
-      if (levels > 0) src_off += levels;
-      clen = (int32_t)((uint32_t)pg.csize - (uint32_t)levels);
-      ulen = (int32_t)((uint32_t)pg.usize - (uint32_t)levels);
-    }
+    if (pg.read_status != kOK || pg.scratch_offset < 0 || !pg.sn_fallback) continue;
+    const SnapLoc L = snap_loc(pg);
     const JobDev job = jobs[pg.job];
-    SnapBlock blk{gconst(job.data) + src_off, clen, gmut(scratch) + job.scratch_base + pg.scratch_offset, ulen, &sh};
-    // decodedLen: binary.Uvarint over the block (decode.go:32-43)
-    uint64_t v = 0;
+    SnapBlock blk{gconst(job.data) + L.src_off, L.clen, gmut(scratch) + job.scratch_base + pg.scratch_offset, L.ulen,
+                  &sh};
     int hl = 0;
-    int e = kOK;
-    {
-      blk.fill(0);
-      unsigned sft = 0;
-      for (int i = 0;; i++) {
-        if (i >= clen) { e = kSNAPPY; break; }
-        const int b = lds_ptr(sh.in)[i - blk.in_base];
-        if (b < 0x80) {
-          if (i > 9 || (i == 9 && b > 1)) e = kSNAPPY;
-          else v |= (sft < 64 ? (uint64_t)b << sft : 0);
-          hl = i + 1;
-          break;
-        }
-        if (sft < 64) v |= (uint64_t)(b & 0x7f) << sft;
-        sft += 7;
-      }
-    }
-    if (e == kOK && v > 0xffffffffull) e = kSNAPPY;
-    if (e == kOK && (int64_t)v != ulen) e = kSIZE;
+    blk.fill(0);
+    int e = snappy_header([&](int i) { return (int)lds_ptr(sh.in)[i - blk.in_base]; }, L.clen, L.ulen, &hl);
     if (e == kOK) e = blk.run(hl);
 #ifdef PQG_PROFILE
     for (int k = 0; k < 16; k++) PQG_ACC(k, 0, blk.pacc[k]);
