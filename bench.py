@@ -211,8 +211,10 @@ def verify(wl, dec, res):
 # ---------------------------------------------------------------- CPU baseline
 def cpu_baseline(wl, seconds):
     """The oracle (C++ restatement of parquet-go's readPages/readPageData) on a
-    bounded sample of the workload's chunks: one thread, then a thread pool
-    over independent chunks (ctypes releases the GIL during the call)."""
+    bounded sample of the workload's chunks: one thread (parquet-go's one
+    goroutine per FileReader, file_reader.go:27-118), then the same sample split
+    into page ranges over a pool of the host's threads (pages decode
+    independently once the dictionary is read; ctypes releases the GIL)."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import pyoracle as O
     from pqgpu import abi
@@ -232,6 +234,13 @@ def cpu_baseline(wl, seconds):
         OL.pqo_free_result(C.byref(r))
         return b
 
+    def run_range(task):
+        job, lo, hi = task
+        b = C.c_int64(0)
+        rc = OL.pqo_decode_page_range(C.byref(job), lo, hi, C.byref(b))
+        assert rc >= 0, rc
+        return b.value
+
     done, t1, k = 0, 0.0, 0
     while k < len(jobs) and t1 < seconds / 2:
         t = time.perf_counter()
@@ -240,18 +249,23 @@ def cpu_baseline(wl, seconds):
         k += 1
     single = done / t1 / 1e9
     cores = host_cores()
-    sample = [jobs[i % len(jobs)] for i in range(min(len(jobs), max(cores, k)))]
+    # the same k chunks, as page ranges: ~4 ranges per thread over all pages
+    tasks = []
+    for job in jobs[:k]:
+        n = int(OL.pqo_decode_page_range(C.byref(job), 0, 0, None))
+        per = max(1, -(-n // max(1, (4 * cores) // k)))
+        tasks += [(job, lo, min(n, lo + per)) for lo in range(0, n, per)]
     t = time.perf_counter()
     with ThreadPoolExecutor(max_workers=cores) as ex:
-        pool_bytes = sum(ex.map(run, sample))
+        pool_bytes = sum(ex.map(run_range, tasks))
     tp = time.perf_counter() - t
-    used = min(cores, len(sample))
     return ({"value": round(single, 4), "unit": "GB/s", "cores": 1, "kind": "port",
              "sample": "oracle (C++ restatement of parquet-go readPages/readPageData) on %d of %d chunks, one thread "
                        "like parquet-go's one-goroutine FileReader; %.1fs" % (k, len(jobs), t1)},
-            {"value": round(pool_bytes / tp / 1e9, 4), "unit": "GB/s", "cores": used, "kind": "port",
-             "sample": "oracle on %d chunks over a pool of %d host threads (independent column chunks); %.1fs"
-                       % (len(sample), used, tp)})
+            {"value": round(pool_bytes / tp / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": "port",
+             "sample": "oracle on the same %d chunks split into %d page ranges over a pool of %d host threads "
+                       "(pages decode independently once the dictionary is read); %.1fs"
+                       % (k, len(tasks), cores, tp)})
 
 
 # ---------------------------------------------------------------- PMC traffic (committed passes)
@@ -283,11 +297,13 @@ def run_workload(wl, dec, args, steps, warmup, barrier, dist, world, rank, cpu_s
     from pqgpu import abi
     L = dec.L
     jobs = []
+    wl.uploaded = 0
     for pf, specs, _ in wl.files:
-        dev = dec.upload(pf.data)
+        # only the selected chunks' byte span goes to HBM (skipChunk, chunk_reader.go:286-312)
+        fj, dev, (lo, hi) = pqgpu.span_jobs(pf, specs, dec)
         wl.devs.append(dev)
-        for (rg, col) in specs:
-            jobs.append(pqgpu.device_job(pf, rg, col, dev))
+        wl.uploaded += hi - lo
+        jobs += fj
     n = len(jobs)
     arr = (abi.ChunkJob * n)(*jobs)
     res = (abi.ChunkResult * n)()
@@ -314,7 +330,8 @@ def run_workload(wl, dec, args, steps, warmup, barrier, dist, world, rank, cpu_s
     elapsed = t_end - t_start
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        on_gpu = dist.get_backend() == "nccl"
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     b_in, b_out, alg = account(wl, dec, res)
@@ -332,6 +349,7 @@ def run_workload(wl, dec, args, steps, warmup, barrier, dist, world, rank, cpu_s
         "chunks_per_step": n,
         "bytes_in": b_in,
         "bytes_out": b_out,
+        "h2d_bytes_per_rank": wl.uploaded,
         "roofline": {
             "bound": "hbm",
             "kernel": "stage " + dom_name + " (" + "+".join(STAGE_KERNELS[dom_name]) + ")",
@@ -425,6 +443,22 @@ def k8_list_c5(dec, wl, res, args):
     return out
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: run this script as N ranks under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) and
+    return their exit code.  Called before this process touches the GPU."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log("launching %d ranks: %s" % (n, " ".join(cmd)))
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -444,15 +478,25 @@ def main():
     ap.add_argument("--only", type=str, default="", help="profiling: run one config alone and print its result")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # nothing above touched the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
     dist = None
+    device = local
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        ndev = torch.cuda.device_count()  # counting devices does not initialise the GPU
+        device = local % max(ndev, 1)
+        torch.cuda.set_device(device)
+        if ndev >= world:  # one GPU per rank: RCCL for the barrier and the max-time reduction
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:  # ranks sharing a GPU (a 1-GPU test box): the same clock over gloo
+            dist.init_process_group("gloo")
 
     def barrier():
         if dist is not None:
@@ -461,7 +505,7 @@ def main():
             dist.barrier()
 
     import pqgpu
-    dec = pqgpu.GpuDecoder(local)
+    dec = pqgpu.GpuDecoder(device)
 
     def release(wl):
         for d in wl.devs:
@@ -472,7 +516,7 @@ def main():
         w = gen_workload(args.only, args, rank, world)
         sub, _ = run_workload(w, dec, args, args.steps, args.warmup, barrier, dist, world, rank, 6.0)
         if rank == 0:
-            print(json.dumps({"only": args.only, **sub}), flush=True)
+            print(json.dumps({"only": args.only, "n_gpus": world, **sub}), flush=True)
         release(w)
         dec.close()
         return

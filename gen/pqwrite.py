@@ -299,7 +299,7 @@ def c5_row_group_columns(rg, rows, seed=5, rows_per_page=20000):
       lst   LIST<double> (3-level; length U{0..3}, 5% null lists, 5% null elements)
       i32   int32 PLAIN          i64d  int64 DELTA_BINARY_PACKED
       f64   double PLAIN         f32   float PLAIN
-      i96   int96 PLAIN          oi32  optional int32 RLE_DICTIONARY (10% nulls)
+      i96   int96 PLAIN          oi32  optional int32 PLAIN (10% nulls, dictionary off: SURVEY §8d)
       s     required string RLE_DICTIONARY (4096-word vocabulary, length U[4,32])
       i64s  int64 PLAIN SNAPPY
     Returns a dict name -> dict(values, def_levels, rep_levels, offsets)."""
@@ -371,7 +371,12 @@ def config_c5(row_groups=(0,), rows_per_rg=C5_ROWS_PER_RG, seed=5, rows_per_page
         Column("f64", DOUBLE, cat("f64", "values"), rows_per_page=rows_per_page),
         Column("f32", FLOAT, cat("f32", "values"), rows_per_page=rows_per_page),
         Column("i96", INT96, cat("i96", "values"), rows_per_page=rows_per_page),
-        Column("oi32", INT32, cat("oi32", "values"), repetition=OPTIONAL, encoding=RLE_DICTIONARY,
+        # the optional int32 column is written with dictionary off
+        # (PLAIN) so that no quirk triggers: Q1 (per-page trailing nils,
+        # chunk_reader.go:394-397) and Q2 (dictionary aliasing of the reused
+        # values array from row group 2 on, chunk_reader.go:235) both need a
+        # multi-page dictionary chunk with nulls
+        Column("oi32", INT32, cat("oi32", "values"), repetition=OPTIONAL, encoding=PLAIN,
                def_levels=cat("oi32", "def_levels"), rows_per_page=rows_per_page),
         Column("s", BYTE_ARRAY, cat("s", "values"), offsets=cat("s", "offsets"), encoding=RLE_DICTIONARY,
                rows_per_page=rows_per_page),

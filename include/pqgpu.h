@@ -380,6 +380,12 @@ typedef struct pqg_chunk_meta {
 /* Parse a whole parquet file held in host memory: PAR1 magic at both ends,
  * footer length, thrift FileMetaData, schema → leaf columns with maxD/maxR. */
 int pqg_file_open(const uint8_t* file, int64_t len, pqg_file** out);
+/* The same from the file's first head_len bytes and its LAST tail_len bytes
+ * (file_len in all): a range reader's footer fetch.  PQG_ERR_INVALID_ARG when
+ * the tail is shorter than the footer + 8 bytes (read the i32 footer length
+ * in the last 8 bytes, then fetch footer + 8). */
+int pqg_file_open_tail(const uint8_t* head, int64_t head_len, const uint8_t* tail, int64_t tail_len, int64_t file_len,
+                       pqg_file** out);
 void pqg_file_close(pqg_file* f);
 int pqg_file_num_columns(const pqg_file* f);
 int pqg_file_num_row_groups(const pqg_file* f);
@@ -418,6 +424,10 @@ typedef struct pqo_store_rg {
 } pqo_store_rg;
 int pqo_decode_column_store(const pqg_chunk_job* jobs, int n_row_groups, int quirks, pqo_store_rg* out);
 void pqo_free_store(pqo_store_rg* out, int n_row_groups);
+/* CPU-baseline helper: decode data pages [page_lo, page_hi) of a chunk (its
+ * dictionary page always), for a thread pool over pages; *out_bytes = output
+ * bytes of those pages.  Returns the number of data pages, or a status < 0. */
+int64_t pqo_decode_page_range(const pqg_chunk_job* job, int page_lo, int page_hi, int64_t* out_bytes);
 /* K8 restatements (host pointers): the ColumnStore.get / getData cursor walks */
 int pqo_assemble(pqg_assemble_args* args);
 int pqo_assemble_list(pqg_list_args* args);

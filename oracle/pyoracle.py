@@ -34,6 +34,8 @@ def lib():
         L.pqo_decode_chunk.argtypes = [C.POINTER(abi.ChunkJob), C.POINTER(abi.ChunkResult),
                                        C.POINTER(abi.PageInfo), C.c_int, C.POINTER(C.c_int)]
         L.pqo_free_result.argtypes = [C.POINTER(abi.ChunkResult)]
+        L.pqo_decode_page_range.argtypes = [C.POINTER(abi.ChunkJob), C.c_int, C.c_int, C.POINTER(C.c_int64)]
+        L.pqo_decode_page_range.restype = C.c_int64
         L.pqo_unpack8_32.argtypes = [C.c_char_p, C.c_int, C.c_void_p]
         L.pqo_unpack8_64.argtypes = [C.c_char_p, C.c_int, C.c_void_p]
         L.pqo_hybrid_decode.argtypes = [C.c_char_p, C.c_int64, C.c_int, C.c_int64, C.c_void_p]

@@ -219,16 +219,32 @@ bool read_schema(const std::vector<Elem>& s, size_t& idx, const std::string& nam
 
 extern "C" {
 
+static int open_footer(const uint8_t* footer, int32_t fl, pqg_file** out);
+
 int pqg_file_open(const uint8_t* file, int64_t len, pqg_file** out) {
   if (!file || !out || len < 0) return PQG_ERR_INVALID_ARG;
+  return pqg_file_open_tail(file, len, file, len, len, out);
+}
+
+// readFileMetaData (file_meta.go:14-62) from the file's first bytes and its
+// last tail_len bytes only: what a range reader fetches before planning.
+int pqg_file_open_tail(const uint8_t* head, int64_t head_len, const uint8_t* tail, int64_t tail_len, int64_t file_len,
+                       pqg_file** out) {
+  if (!head || !tail || !out || head_len < 0 || tail_len < 0 || file_len < 0 || tail_len > file_len)
+    return PQG_ERR_INVALID_ARG;
   *out = nullptr;
-  if (len < 4 || memcmp(file, "PAR1", 4) != 0) return PQG_ERR_METADATA;
-  if (len < 8 || memcmp(file + len - 4, "PAR1", 4) != 0) return PQG_ERR_METADATA;
+  if (head_len < 4 || memcmp(head, "PAR1", 4) != 0) return PQG_ERR_METADATA;
+  if (tail_len < 8 || memcmp(tail + tail_len - 4, "PAR1", 4) != 0) return PQG_ERR_METADATA;
   int32_t fl;
-  memcpy(&fl, file + len - 8, 4);
+  memcpy(&fl, tail + tail_len - 8, 4);
   if (fl <= 0) return PQG_ERR_METADATA;
-  if ((int64_t)fl + 8 > len) return PQG_ERR_METADATA;
-  Parser P(file + len - 8 - fl, fl);
+  if ((int64_t)fl + 8 > file_len) return PQG_ERR_METADATA;
+  if ((int64_t)fl + 8 > tail_len) return PQG_ERR_INVALID_ARG;  // fetch the last fl + 8 bytes
+  return open_footer(tail + tail_len - 8 - fl, fl, out);
+}
+
+static int open_footer(const uint8_t* footer, int32_t fl, pqg_file** out) {
+  Parser P(footer, fl);
   std::vector<Elem> schema;
   std::vector<std::vector<ChunkM>> rgs;
   std::vector<int64_t> rg_rows;

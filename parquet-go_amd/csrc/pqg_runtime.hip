@@ -51,8 +51,6 @@ __global__ void k_snap_link(const JobDev* jobs, PageDev* pages, const int* list,
                             const uint2* F);
 __global__ void k_snap_decode(const JobDev* jobs, PageDev* pages, const SnapSub* subs, const int* sub_total,
                               int sub_cap, int* queue, uint8_t* scratch);
-__global__ void k_snap_wg(const JobDev* jobs, PageDev* pages, const SnapSub* subs, const int* sub_total, int sub_cap,
-                          int* queue, uint8_t* scratch);
 __global__ void k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                               uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena);
 __global__ void k_hybrid_walk(const PageDev* pages, const int* list, const int* total, HStream* streams,
@@ -416,13 +414,8 @@ static void launch_snappy(pqg_ctx* c, hipStream_t s, JobDev* jobs, PageDev* page
                      dim3(256), 0, s, jobs, pages, list, total, sctr, T.subs, T.sub_cap, T.segpage, T.seg_cap);
   hipLaunchKernelGGL(k_snap_seg, dim3(c->num_cus * 16), dim3(64), 0, s, jobs, pages, T.segpage, sctr + 1, T.seg_cap, T.F);
   hipLaunchKernelGGL(k_snap_link, dim3(c->num_cus * 4), dim3(64), 0, s, jobs, pages, list, total, T.subs, T.F);
-#ifdef PQG_SNAP_WAVE  // experiment build: one wave per sub-block, 16 KiB LDS ring + L2 history
   hipLaunchKernelGGL(k_snap_decode, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, T.subs, sctr, T.sub_cap, q_split,
                      scratch);
-#else  // one 512-thread workgroup per sub-block, its 64 KiB output in LDS (one per CU)
-  hipLaunchKernelGGL(k_snap_wg, dim3(qgrid(c->num_cus)), dim3(512), 0, s, jobs, pages, T.subs, sctr, T.sub_cap,
-                     q_split, scratch);
-#endif
   hipLaunchKernelGGL(k_snappy, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, total, q_serial, scratch);
 }
 

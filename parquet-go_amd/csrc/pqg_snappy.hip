@@ -50,7 +50,10 @@ int prof_read_snappy(unsigned long long* out) {
 // literal longer than the window goes from HBM in 4 KiB pieces.
 // ============================================================================
 constexpr int kPos = 128;         // tag positions parsed per window (2 per lane)
-constexpr int kDense = 4;         // tags in a window for the batched byte resolution
+#ifndef PQG_SNAPPY_DENSE
+#define PQG_SNAPPY_DENSE 4
+#endif
+constexpr int kDense = PQG_SNAPPY_DENSE;  // tags in a window for the batched byte resolution
 constexpr int kSnWin = 4096;      // compressed-stream window (LDS)
 constexpr int kSnWinNeed = 2048;  // window bytes wanted ahead of the first tag
 constexpr int kSpan = 1024;       // output bytes a batch covers: 64 lanes x one 16-byte granule
@@ -1035,428 +1038,6 @@ __global__ void __launch_bounds__(64) k_snap_decode(const JobDev* jobs, PageDev*
     for (int k = 0; k < 16; k++) PQG_ACC(k, 0, blk.pacc[k]);
 #endif
     if (why && lane == 0) atomicOr(&pages[sb.page].sn_fallback, why);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// k_snap_wg: one 512-thread workgroup per 64 KiB sub-block, its output held
-// in LDS (every copy of the sub-block reads it there).  The compressed
-// stream is taken kChunkPos positions at a time (a "chunk"):
-//  1. the chunk's bytes are staged in LDS;
-//  2. each wave parses 4 windows of 64 positions (one tag per lane,
-//     speculatively); six ds_bpermute doubling rounds give every position its
-//     exit from the window, the output bytes on the way and the 64-bit set of
-//     window positions on its chain; lanes then walk the wave's 4 windows
-//     from each of the group's first 64 positions (near entries);
-//  3. wave 0 links the 8 groups (one LDS read per group; an entry further
-//     into a group, after a long literal, hops its windows);
-//  4. every wave marks its windows' chain tags and scans their output bytes;
-//  5. the reference's checks (decode_other.go:45-99) on every chain tag; the
-//     sub-block's end and the chunk's output cap cut the chunk;
-//  6. the chunk's output bytes are resolved one per thread-slot: a literal byte
-//     from the staged input, a copy byte from the output already in LDS, or,
-//     when its source is in the same chunk, by pointer doubling over the
-//     chunk; then stored into the LDS output.
-// The finished sub-block leaves for HBM as 16-byte stores.
-// ---------------------------------------------------------------------------
-constexpr int kWgThreads = 512;
-constexpr int kWgWaves = kWgThreads / 64;
-constexpr int kChunkPos = kWgWaves * 256;  // 4 windows of 64 positions per wave
-constexpr int kOcap = 4096;                // output bytes resolved per chunk (8 per thread)
-constexpr int kInStage = kChunkPos + 128;
-constexpr uint32_t kNoCut = 0xffffu;
-
-struct WgShared {
-  uint8_t out[kSnapSub + 64];
-  uint8_t in[kInStage + 16];
-  uint2 gex[kWgWaves][64];     // near-entry group exits: {exit (chunk-relative), output bytes}
-  uint2 xo[kChunkPos];         // per position: exit from its window (chunk-relative), output bytes
-  uint16_t tm[kOcap];          // 1 + position of the tag whose output starts at this byte
-  uint32_t tinfo[kChunkPos];   // per chain tag: literal 0x80000000 | its data position; copy: offset
-  uint32_t tstart[kChunkPos];  // per chain tag: output start, chunk-relative
-  int32_t src[kOcap];          // byte resolution: 0x80000000 | value, or the chunk byte it copies
-  uint32_t win_out[4 * kWgWaves];
-  uint32_t win_off[4 * kWgWaves + 1];
-  int32_t gentry[kWgWaves];
-  uint32_t scan[kWgWaves];
-  int32_t item, cut, fail, cexit;
-};
-
-__device__ __forceinline__ uint32_t dpp_incl_max_u(uint32_t x) { return dpp_incl_max(x); }
-
-// phase timers of k_snap_wg (diagnostic builds): thread 0 adds s_memtime deltas to pqg_prof[16..31]
-#ifdef PQG_PROFILE
-#define WG_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#define WG_A(slot, a, b) \
-  do { if (threadIdx.x == 0) atomicAdd(&pqg_prof[slot], (unsigned long long)((b) - (a))); } while (0)
-#define WG_N(slot) do { if (threadIdx.x == 0) atomicAdd(&pqg_prof[slot], 1ull); } while (0)
-#else
-#define WG_T(v)
-#define WG_A(slot, a, b) do { } while (0)
-#define WG_N(slot) do { } while (0)
-#endif
-
-__global__ void __launch_bounds__(kWgThreads) k_snap_wg(const JobDev* jobs, PageDev* pages, const SnapSub* subs,
-                                                        const int* sub_total, int sub_cap, int* queue,
-                                                        uint8_t* scratch) {
-  __shared__ __attribute__((aligned(16))) WgShared S;
-  const int tid = (int)threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const int n_items = min(*sub_total, sub_cap);
-  for (;;) {
-    if (tid == 0) S.item = queue_pull(queue);
-    __syncthreads();
-    const int t = S.item;
-    if (t >= n_items) return;
-    const SnapSub sb = subs[t];
-    const PageDev pg = pages[sb.page];
-    if (pg.sn_fallback || sb.pos < 0) {
-      __syncthreads();  // S.item is rewritten next
-      continue;
-    }
-    const JobDev job = jobs[pg.job];
-    const SnapLoc L = snap_loc(pg);
-    gcu8 src = gconst(job.data) + L.src_off;
-    const int64_t slen = L.clen;
-    const int64_t base = (int64_t)sb.j * kSnapSub;
-    const int64_t dend = base + kSnapSub < L.ulen ? base + kSnapSub : L.ulen;
-    const bool lastsub = dend == L.ulen;
-    WG_T(t_sub0);
-    WG_N(29);
-    int64_t c0 = sb.pos;            // block position of the chunk's first tag (a chain tag)
-    int64_t od = sb.out;            // its output offset in the page
-    bool fail = false;
-    // ---- per chunk
-    while (!fail) {
-      const bool skip = od < base;  // still walking to the sub-block's first tag: no output
-      if (!skip && !lastsub && od >= dend) break;
-      if (c0 >= slen) {
-        fail = !lastsub || od != dend;
-        break;
-      }
-      WG_T(p0);
-      // 1. stage [c0, c0 + kInStage) (aligned dwords holding no block byte read 0)
-      {
-        const uintptr_t a0 = (uintptr_t)(src + c0), end = (uintptr_t)(src + slen);
-        const uint32_t sft = (uint32_t)(a0 & 3) * 8;
-        for (int g = tid; g < kInStage / 4; g += kWgThreads) {
-          const uintptr_t q = (a0 & ~(uintptr_t)3) + 4 * (uintptr_t)g;
-          const uint32_t w0 = q < end ? *(const PQG_G uint32_t*)q : 0u;
-          const uint32_t w1 = q + 4 < end ? *(const PQG_G uint32_t*)(q + 4) : 0u;
-          *(PQG_L uint32_t*)(lds_ptr(S.in) + 4 * g) = __builtin_amdgcn_alignbit(w1, w0, sft);
-        }
-      }
-      if (tid == 0) {
-        S.cut = (int)kNoCut;
-        S.fail = 0;
-      }
-      __syncthreads();
-      WG_T(p1);
-      WG_A(16, p0, p1);
-      // 2. four windows per wave
-      uint32_t J[4], O[4], Rl[4], Rh[4], len[4], inf[4];
-      uint64_t V[4];  // positions inside the block (a tag can start there)
-      bool lit[4], err[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int pl = 256 * w + 64 * k + lane;  // chunk-relative position
-        const int64_t p = c0 + pl;
-        const Tag tg = parse_tag(lds_ptr(S.in), (uint32_t)pl, p, slen, lane);
-        len[k] = (uint32_t)(tg.len < (1 << 30) ? tg.len : (1 << 30));
-        lit[k] = tg.lit;
-        err[k] = tg.err;
-        inf[k] = tg.lit ? (uint32_t)(pl + tg.hdr) : tg.info;
-        uint32_t j = tg.next < 0x7fffffff ? (uint32_t)tg.next : 0x7fffffffu;  // window-relative
-        uint32_t o = len[k];
-        V[k] = __ballot(p < slen);
-        if (p >= slen) {  // no tag at or past the end: a fixed point
-          j = (uint32_t)lane;
-          o = 0;
-        }
-        uint32_t rl = lane < 32 ? 1u << lane : 0u, rh = lane >= 32 ? 1u << (lane - 32) : 0u;
-#pragma unroll
-        for (int r = 0; r < 6; r++) {
-          const bool in = j < 64;
-          const int from = in ? (int)j : lane;
-          const uint32_t jn = bperm(j, from), on = bperm(o, from), ln = bperm(rl, from), hn = bperm(rh, from);
-          if (in && j != (uint32_t)lane) {
-            j = jn;
-            o = sat_add(o, on);
-            rl |= ln;
-            rh |= hn;
-          }
-        }
-        J[k] = j;
-        O[k] = o;
-        Rl[k] = rl;
-        Rh[k] = rh;
-        // window exit, chunk-relative (a fixed point stays itself)
-        const uint32_t xe = j == (uint32_t)lane ? (uint32_t)pl : sat_add((uint32_t)(pl - lane), j);
-        S.xo[pl] = make_uint2(xe, o);
-      }
-      // near entries of the group: walk its 4 windows
-      {
-        uint32_t x = (uint32_t)lane, acc = 0;  // group-relative
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const bool in = (x >> 6) == (uint32_t)k;
-          const int from = in ? (int)(x & 63) : lane;
-          const uint32_t jx = bperm(J[k], from), ox = bperm(O[k], from);
-          if (in) {
-            x = jx == (uint32_t)from && jx < 64 ? 64 * k + jx : sat_add(64u * k, jx);
-            acc = sat_add(acc, ox);
-          }
-        }
-        S.gex[w][lane] = make_uint2(sat_add(x, 256u * w), acc);
-      }
-      __syncthreads();
-      WG_T(p2);
-      WG_A(17, p1, p2);
-      // 3. link the groups (wave 0)
-      if (w == 0) {
-        uint32_t x = 0;
-        for (int g = 0; g < kWgWaves; g++) {
-          int ge = -1;
-          if (x >= 256u * g && x < 256u * (g + 1)) {
-            ge = (int)x;
-            const uint32_t rel = x - 256u * g;
-            if (rel < 64) {
-              x = S.gex[g][rel].x;
-            } else {  // entered past the near entries (after a long literal): hop the windows
-              uint32_t y = x;
-              for (int h = 0; h < 4 && y < 256u * (g + 1); h++) {
-                const uint32_t ny = S.xo[y].x;
-                if (ny == y) break;
-                y = ny;
-              }
-              x = y;
-            }
-          }
-          if (lane == 0) S.gentry[g] = ge;
-        }
-        if (lane == 0) S.cexit = (int)(x < 0x7fffffffu ? x : 0x7fffffffu);
-      }
-      __syncthreads();
-      WG_T(p3);
-      WG_A(18, p2, p3);
-      // 4. this wave's chain tags and their output offsets
-      uint64_t M[4];
-      {
-        const int ge = S.gentry[w];
-        uint32_t x = ge < 0 ? 0xffffffffu : (uint32_t)(ge - 256 * w);
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          M[k] = 0;
-          uint32_t osum = 0;
-          if ((x >> 6) == (uint32_t)k) {
-            const int e = (int)(x & 63);
-            M[k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)Rl[k], e) |
-                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)Rh[k], e) << 32) &
-                   V[k];
-            osum = (uint32_t)__builtin_amdgcn_readlane((int)O[k], e);
-            const uint32_t je = (uint32_t)__builtin_amdgcn_readlane((int)J[k], e);
-            x = je == (uint32_t)e ? 0xffffffffu : sat_add(64u * k, je);  // a fixed point ends the chain
-          }
-          if (lane == 0) S.win_out[4 * w + k] = osum;
-        }
-      }
-      __syncthreads();
-      if (w == 0) {  // exclusive scan of the window outputs (chain order = window order)
-        const uint32_t v = lane < 4 * kWgWaves ? S.win_out[lane] : 0u;
-        const uint32_t inc = dpp_incl_add(v);
-        if (lane < 4 * kWgWaves) S.win_off[lane] = inc - v;
-        if (lane == 4 * kWgWaves - 1) S.win_off[4 * kWgWaves] = inc;
-      }
-      __syncthreads();
-      WG_T(p4);
-      WG_A(19, p3, p4);
-      // 5. checks and the cut
-      const int64_t D = od - base;  // chunk output start, sub-block relative (< 0 while skipping)
-      uint32_t dtr[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const bool m = (M[k] >> lane) & 1;
-        const uint32_t v = m ? len[k] : 0u;
-        dtr[k] = S.win_off[4 * w + k] + (dpp_incl_add(v) - v);
-        if (m) {
-          const int pl = 256 * w + 64 * k + lane;
-          const int64_t T = D + (int64_t)dtr[k];  // tag output start, sub-block relative
-          bool cut = false;
-          if (skip) {
-            cut = T >= 0;  // the sub-block's first tag
-          } else {
-            cut = (!lastsub && base + T >= dend) || (int64_t)dtr[k] + len[k] > kOcap;
-          }
-          if (cut) atomicMin(&S.cut, pl);
-          S.tstart[pl] = dtr[k];
-        }
-      }
-      __syncthreads();
-      const int cut = S.cut;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const bool m = (M[k] >> lane) & 1;
-        const int pl = 256 * w + 64 * k + lane;
-        if (m && pl < cut) {
-          const int64_t T = D + (int64_t)dtr[k];
-          bool e;
-          if (skip) {
-            e = T + (int64_t)len[k] > 0;  // straddles the sub-block start
-          } else {
-            e = err[k] || (int64_t)len[k] > (dend - base) - T;      // length > len(dst)-d
-            if (!lit[k]) e |= inf[k] == 0 || (int64_t)inf[k] > T;  // offset <= 0 || d < offset
-            else S.tinfo[pl] = 0x80000000u | inf[k];
-            if (!lit[k]) S.tinfo[pl] = inf[k];
-          }
-          if (e) S.fail = 1;
-        }
-      }
-      __syncthreads();
-      WG_T(p5);
-      WG_A(20, p4, p5);
-      if (S.fail) {
-        fail = true;
-        break;
-      }
-      // chunk output [D, D1) and the next chunk's first tag
-      int64_t D1, next;
-      if (cut != (int)kNoCut) {
-        D1 = D + (int64_t)S.tstart[cut];
-        next = c0 + cut;
-      } else {
-        D1 = D + (int64_t)S.win_off[4 * kWgWaves];
-        next = c0 + S.cexit;
-      }
-      if (skip) {
-        WG_N(27);
-        if (cut != (int)kNoCut && D1 != 0) fail = true;  // chain tags never start exactly at base
-        od = base + D1;
-        c0 = next;
-        __syncthreads();
-        continue;
-      }
-      if (cut == 0) {
-        // the first tag alone exceeds the output cap: a long literal, copied from HBM
-        const Tag tg = parse_tag(lds_ptr(S.in), 0, c0, slen, 0);
-        const int64_t ln = tg.len;
-        if (!tg.lit || tg.err || ln > (dend - base) - D) {
-          fail = true;
-          break;
-        }
-        for (int64_t i = tid; i < ln; i += kWgThreads) S.out[D + i] = src[c0 + tg.hdr + i];
-        od += ln;
-        c0 += tg.hdr + ln;
-        __syncthreads();
-        WG_T(p6);
-        WG_A(24, p5, p6);
-        WG_N(30);
-        continue;
-      }
-      // 6. resolve the chunk's output bytes
-      const int n = (int)(D1 - D);
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const int i = 8 * tid + q;
-        if (i < kOcap) S.tm[i] = 0;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const bool m = (M[k] >> lane) & 1;
-        const int pl = 256 * w + 64 * k + lane;
-        if (m && pl < cut) S.tm[dtr[k]] = (uint16_t)(pl + 1);
-      }
-      __syncthreads();
-      uint32_t tix[8];
-      uint32_t run = 0;
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const uint32_t mk = S.tm[8 * tid + q];
-        run = mk > run ? mk : run;
-        tix[q] = run;
-      }
-      // exclusive max over the threads before: wave scan, then the waves before
-      const uint32_t wmax = dpp_incl_max_u(run);
-      if (lane == 63) S.scan[w] = wmax;
-      __syncthreads();
-      uint32_t before = dpp_prev(wmax);
-      for (int v = 0; v < w; v++) before = S.scan[v] > before ? S.scan[v] : before;
-      int32_t rs[8];
-      bool pend = false;
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const int i = 8 * tid + q;
-        rs[q] = (int32_t)0x80000000;
-        if (i < n) {
-          const uint32_t tp = (tix[q] > before ? tix[q] : before) - 1;
-          const uint32_t info = S.tinfo[tp];
-          const int st = (int)S.tstart[tp];
-          if (info & 0x80000000u) {
-            const int64_t qd = (int64_t)(info & 0x7fffffffu) + (i - st);
-            const uint32_t b = qd < kInStage ? (uint32_t)S.in[qd] : (uint32_t)src[c0 + qd];
-            rs[q] = (int32_t)(0x80000000u | b);
-          } else {
-            const int64_t sidx = D + i - (int64_t)info;  // sub-block relative source
-            if (sidx < D) rs[q] = (int32_t)(0x80000000u | (uint32_t)S.out[sidx]);
-            else {
-              rs[q] = (int32_t)(sidx - D);
-              pend = true;
-            }
-          }
-        }
-        if (i < kOcap) S.src[i] = rs[q];
-      }
-      __syncthreads();
-      WG_T(p7);
-      WG_A(21, p5, p7);
-      WG_N(26);
-      while (__syncthreads_or(pend)) {
-        WG_N(28);
-        pend = false;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          if (rs[q] >= 0) {
-            rs[q] = S.src[rs[q]];
-            pend |= rs[q] >= 0;
-          }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          const int i = 8 * tid + q;
-          if (i < kOcap) S.src[i] = rs[q];
-        }
-        __syncthreads();
-      }
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const int i = 8 * tid + q;
-        if (i < n) S.out[D + i] = (uint8_t)(rs[q] & 0xff);
-      }
-      WG_T(p8);
-      WG_A(22, p7, p8);
-      od = base + D1;
-      c0 = next;
-      __syncthreads();
-      WG_T(p9);
-      WG_A(23, p8, p9);
-    }
-    WG_T(t_fl0);
-    // ---- the sub-block to HBM, or the page to the serial path
-    const int64_t nb = dend - base;
-    if (!fail && od != dend) fail = true;
-    if (fail) {
-      if (tid == 0) atomicOr(&pages[sb.page].sn_fallback, 256);
-    } else {
-      PQG_G uint8_t* dst = gmut(scratch) + job.scratch_base + pg.scratch_offset + base;
-      for (int64_t g = 16 * tid; g < nb; g += 16 * kWgThreads) {
-        const u32x4_t v = *(const PQG_L u32x4_t*)(lds_ptr(S.out) + g);
-        stg16((uintptr_t)(dst + g), make_uint4(v.x, v.y, v.z, v.w));
-      }
-    }
-    __syncthreads();
-    WG_T(t_fl1);
-    WG_A(25, t_fl0, t_fl1);
-    WG_A(31, t_sub0, t_fl1);
   }
 }
 

@@ -10,6 +10,7 @@ Column projection follows schema.isSelected (schema.go:296-312): an empty
 selection reads every column.
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -29,15 +30,36 @@ def _check(rc, what):
 
 
 class ParquetFile:
-    """Footer + schema of a file held in host memory (readFileMetaData file_meta.go:14-62)."""
+    """Footer + schema of a parquet file (readFileMetaData file_meta.go:14-62).
 
-    def __init__(self, data):
-        self.data = bytes(data)
-        self._buf = np.frombuffer(self.data, dtype=np.uint8)
-        h = C.c_void_p()
-        _check(lib().pqg_file_open(self.data, len(self.data), C.byref(h)), "pqg_file_open")
-        self._h = h
+    ParquetFile(data) holds the whole file in host memory; ParquetFile.open(path)
+    reads only the first 4 bytes and the footer, and chunk bytes are fetched by
+    byte range on demand (read_range), as readChunk seeks to each chunk
+    (chunk_reader.go:332-340)."""
+
+    def __init__(self, data=None, *, _path=None):
         L = lib()
+        h = C.c_void_p()
+        self.path = _path
+        if _path is None:
+            self.data = bytes(data)
+            self._buf = np.frombuffer(self.data, dtype=np.uint8)
+            self.size = len(self.data)
+            _check(L.pqg_file_open(self.data, len(self.data), C.byref(h)), "pqg_file_open")
+        else:
+            self.data = None
+            self._buf = None
+            self.size = os.path.getsize(_path)
+            with open(_path, "rb") as f:
+                head = f.read(4)
+                f.seek(max(0, self.size - 8))
+                last8 = f.read(8)
+                fl = int.from_bytes(last8[:4], "little", signed=True) if len(last8) == 8 else 0
+                n = min(self.size, max(fl, 0) + 8)
+                f.seek(self.size - n)
+                tail = f.read(n)
+            _check(L.pqg_file_open_tail(head, len(head), tail, len(tail), self.size, C.byref(h)), "pqg_file_open_tail")
+        self._h = h
         self.num_columns = L.pqg_file_num_columns(h)
         self.num_row_groups = L.pqg_file_num_row_groups(h)
         self.num_rows = L.pqg_file_num_rows(h)
@@ -46,6 +68,23 @@ class ParquetFile:
             ci = abi.ColumnInfo()
             _check(L.pqg_file_column(h, i, C.byref(ci)), "pqg_file_column")
             self.columns.append(ci)
+
+    @classmethod
+    def open(cls, path):
+        return cls(_path=path)
+
+    def read_range(self, lo, hi):
+        """Bytes [lo, hi) of the file (shorter at its end)."""
+        lo, hi = max(0, lo), min(hi, self.size)
+        if hi <= lo:
+            return np.zeros(0, np.uint8)
+        if self.path is None:
+            return self._buf[lo:hi]
+        fd = os.open(self.path, os.O_RDONLY)
+        try:
+            return np.frombuffer(os.pread(fd, hi - lo, lo), dtype=np.uint8)
+        finally:
+            os.close(fd)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -73,9 +112,15 @@ class ParquetFile:
         job = abi.ChunkJob()
         job.col = self.columns[col].desc
         job.col.codec = m.codec
-        start = max(0, min(m.start, len(self.data)))
-        job.data = self._buf.ctypes.data + start
-        job.data_len = len(self.data) - start
+        start = max(0, min(m.start, self.size))
+        if self.path is None:
+            job.data = self._buf.ctypes.data + start
+            job.data_len = self.size - start
+        else:  # the chunk's own bytes, kept alive with the file object
+            b = np.ascontiguousarray(self.read_range(start, start + m.total_compressed_size))
+            self._keep = getattr(self, "_keep", []) + [b]
+            job.data = b.ctypes.data if b.nbytes else None
+            job.data_len = b.nbytes
         job.total_compressed_size = m.total_compressed_size
         job.data_page_offset = m.data_page_offset - m.start
         job.num_values_hint = m.num_values
@@ -238,16 +283,64 @@ def device_job(pf: ParquetFile, rg, col, dev_ptr_of_file):
     return job
 
 
-class FileReader:
-    """Mirror of parquet-go's FileReader (file_reader.go): selected columns of a
-    file, decoded one row group at a time on the GPU."""
+def chunk_span(pf: ParquetFile, specs):
+    """The byte span [lo, hi) covering the chunks of (rg, col) pairs
+    ([start, start + TotalCompressedSize) each, chunk_reader.go:332-340) and
+    their ChunkMetas."""
+    metas = [pf.chunk_meta(rg, c) for rg, c in specs]
+    lo = min(m.start for m in metas)
+    hi = max(m.start + m.total_compressed_size for m in metas)
+    return max(0, lo), min(hi, pf.size), metas
 
-    def __init__(self, data, *columns, device=0, decoder=None):
-        self.file = ParquetFile(data)
+
+def span_jobs(pf: ParquetFile, specs, dec):
+    """Chunk jobs for (rg, col) pairs with only their byte span uploaded to one
+    device buffer, each job pointing into it.  Unselected chunks are never
+    read, as skipChunk seeks past them (chunk_reader.go:286-312).  Returns
+    (jobs, device pointer of the span, (lo, hi))."""
+    lo, hi, metas = chunk_span(pf, specs)
+    span = np.ascontiguousarray(pf.read_range(lo, hi))
+    dev = dec.upload(span)
+    jobs = []
+    for (rg, c), m in zip(specs, metas):
+        job = abi.ChunkJob()
+        job.col = pf.columns[c].desc
+        job.col.codec = m.codec
+        job.total_compressed_size = m.total_compressed_size
+        job.data_page_offset = m.data_page_offset - m.start
+        job.num_values_hint = m.num_values
+        job.total_uncompressed_size = m.total_uncompressed_size
+        job.has_dict_page_offset = m.has_dict_page_offset
+        start = max(lo, min(m.start, lo + span.nbytes))
+        job.data = dev + (start - lo)
+        job.data_len = lo + span.nbytes - start  # readable bytes: to the span's end
+        jobs.append(job)
+    return jobs, dev, (lo, lo + span.nbytes)
+
+
+class FileReader:
+    """Mirror of parquet-go's FileReader (file_reader.go:27-118): the selected
+    columns of a file (dotted paths, schema.isSelected schema.go:296-312; none =
+    all), decoded one row group at a time on the GPU.  `source` is the file's
+    bytes or a path; each row group uploads only its selected chunks' byte span
+    (span_jobs)."""
+
+    def __init__(self, source, *columns, device=0, decoder=None):
+        self.file = ParquetFile.open(source) if isinstance(source, (str, os.PathLike)) else ParquetFile(source)
         self.dec = decoder or GpuDecoder(device)
-        self._dev = self.dec.upload(self.file.data)
-        self.selected = [self.file.column_index(c) for c in columns] if columns else list(range(self.file.num_columns))
+        self.selected = self._select(columns)
         self.row_group_position = 0
+        self.uploaded_bytes = 0   # H2D bytes so far (projection pushdown check)
+
+    def _select(self, columns):
+        if not columns:
+            return list(range(self.file.num_columns))
+        out = []
+        for i, c in enumerate(self.file.columns):
+            path = c.path.decode()
+            if any(path == p or path.startswith(p + ".") for p in columns):
+                out.append(i)
+        return out
 
     def row_group_count(self):
         return self.file.num_row_groups
@@ -255,14 +348,34 @@ class FileReader:
     def num_rows(self):
         return self.file.num_rows
 
+    def decode_row_groups(self, rgs):
+        """readRowGroup (chunk_reader.go:404-431) for the selected columns of
+        every row group in `rgs`, one batched decode: [(rg, col, ChunkResult)]
+        with device outputs (valid until the next decode on the decoder)."""
+        specs = [(rg, c) for rg in rgs for c in self.selected]
+        if not specs:
+            return []
+        jobs, dev, (lo, hi) = span_jobs(self.file, specs, self.dec)
+        self.uploaded_bytes += hi - lo
+        try:
+            res = self.dec.decode_jobs(jobs)
+        finally:
+            self.dec.free(dev)
+        return [(rg, c, r) for (rg, c), r in zip(specs, res)]
+
     def read_row_group(self, rg):
-        """readRowGroup (chunk_reader.go:404-431) for the selected columns."""
-        jobs = [device_job(self.file, rg, c, self._dev) for c in self.selected]
-        res = self.dec.decode_jobs(jobs)
-        out = {}
-        for i, (c, r) in enumerate(zip(self.selected, res)):
-            out[self.file.columns[c].path.decode()] = self.dec.download(r, i)
-        return out
+        """One row group's selected columns, downloaded: {path: DecodedColumn}."""
+        specs = [(rg, c) for c in self.selected]
+        if not specs:
+            return {}
+        jobs, dev, (lo, hi) = span_jobs(self.file, specs, self.dec)
+        self.uploaded_bytes += hi - lo
+        try:
+            res = self.dec.decode_jobs(jobs)
+            return {self.file.columns[c].path.decode(): self.dec.download(r, i)
+                    for i, ((_, c), r) in enumerate(zip(specs, res))}
+        finally:
+            self.dec.free(dev)
 
     def close(self):
-        self.dec.free(self._dev)
+        pass

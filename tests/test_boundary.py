@@ -196,3 +196,31 @@ def test_unsigned_flag_reaches_result(dec):
             assert outs[0].values.tobytes() == outs[1].values.tobytes()
     finally:
         dec.free(dev)
+
+
+@pytest.mark.gpu
+def test_file_reader_projection_uploads_selected_span(tmp_path):
+    """pqgpu.FileReader (NewFileReader(r, columns...) file_reader.go:27-48,
+    isSelected schema.go:296-312): a path-backed reader uploads only the selected
+    chunks' byte span per row group and decodes them like the oracle."""
+    import pqgpu
+    data, _ = W.config_c5(row_groups=(0, 1), rows_per_rg=6000, rows_per_page=2000)
+    path = tmp_path / "c5.parquet"
+    path.write_bytes(data)
+    pf = pqgpu.ParquetFile(data)
+    dec = pqgpu.GpuDecoder(0)
+    try:
+        fr = pqgpu.FileReader(str(path), "i64d", "s", decoder=dec)
+        sel = [pf.column_index("i64d"), pf.column_index("s")]
+        assert fr.selected == sel
+        for rg in range(2):
+            got = fr.read_row_group(rg)
+            assert sorted(got) == ["i64d", "s"]
+            for c in sel:
+                P.compare_chunk(P.oracle_chunk(pf, rg, c), got[pf.columns[c].path.decode()], "rg%d col%d" % (rg, c))
+        spans = [pqgpu.chunk_span(pf, [(rg, c) for c in sel]) for rg in range(2)]
+        assert fr.uploaded_bytes == sum(hi - lo for lo, hi, _ in spans) < len(data) // 2
+        lst = pqgpu.FileReader(str(path), "lst", decoder=dec)  # a group prefix selects its leaves
+        assert [pf.columns[c].path.decode() for c in lst.selected] == ["lst.list.element"]
+    finally:
+        dec.close()

@@ -80,3 +80,29 @@ def test_planner_unsigned_flag():
     for i in range(pf.num_columns):
         ch = O.decode_chunk(pf.host_job(0, i)[0])
         assert ch.status == 0 and ch.col_flags == pf.columns[i].desc.flags
+
+
+def test_planner_footer_only_open(tmp_path):
+    """pqg_file_open_tail (readFileMetaData file_meta.go:14-62 from the head and
+    the footer only) plans exactly what pqg_file_open plans from the whole file;
+    a range reader's chunk spans cover only the selected chunks."""
+    data, _ = W.config_c5(row_groups=(0, 1, 2), rows_per_rg=2000, rows_per_page=700)
+    path = tmp_path / "f.parquet"
+    path.write_bytes(data)
+    a, b = pqgpu.ParquetFile(data), pqgpu.ParquetFile.open(str(path))
+    assert (a.num_columns, a.num_row_groups, a.num_rows) == (b.num_columns, b.num_row_groups, b.num_rows)
+    for rg in range(3):
+        for c in range(a.num_columns):
+            assert bytes(a.chunk_meta(rg, c)) == bytes(b.chunk_meta(rg, c))
+            m = b.chunk_meta(rg, c)
+            assert bytes(b.read_range(m.start, m.start + m.total_compressed_size)) == \
+                data[m.start:m.start + m.total_compressed_size]
+    lo, hi, _ = pqgpu.chunk_span(b, [(1, c) for c in range(b.num_columns)])
+    assert 4 < lo and hi < b.size - 8  # row group 1 alone: neither neighbour is read
+    L = _lib.lib()
+    import ctypes as C
+    h = C.c_void_p()
+    assert L.pqg_file_open_tail(data[:4], 4, data[-8:], 8, len(data), C.byref(h)) == \
+        pqgpu.abi.STATUS_CODES["INVALID_ARG"]  # the tail must hold the footer
+    assert L.pqg_file_open_tail(b"PAR2", 4, data, len(data), len(data), C.byref(h)) == \
+        pqgpu.abi.STATUS_CODES["METADATA"]

@@ -2,11 +2,14 @@
 independently per rank reproduce the single-process decode, with no collective
 other than the barrier and the timing reduction.
 
-The ranks build their work exactly as bench.py does (bench.gen_workload:
-pqgpu.shard.row_groups_for_rank over the C5 row groups, each generated from
-its global index).  On CPU (gloo, world size 2) each rank decodes its shard
-with the oracle; the GPU variant (-m gpu) runs both ranks on cuda:0 and
-decodes through pqg_decode_chunks, as bench.py does per GPU."""
+All ranks open ONE C5 file (8 x world row groups) by path: each reads the
+footer only, takes its row groups (pqgpu.shard.row_groups_for_rank) and reads
+just their byte span (pqgpu.chunk_span / span_jobs, the skipChunk seek of
+chunk_reader.go:286-312 for everything else).  On CPU (gloo, world size 2)
+each rank decodes its shard with the oracle; the GPU variant (-m gpu) runs both
+ranks on cuda:0 through pqgpu.FileReader (span upload + pqg_decode_chunks).
+bench.gen_workload's per-rank C5 generation is checked to produce the same
+chunk bytes as the one file's row groups."""
 import argparse
 import hashlib
 import os
@@ -45,35 +48,33 @@ def _oracle_digest(job):
     return _digest(r.status, r.num_slots, r.num_values, (r.def_levels, r.rep_levels, r.values, r.offsets))
 
 
-def _decode_shard(rank, world, gpu):
-    """This rank's C5 shard, built and decoded the way bench.py builds it:
-    {(global rg, col): digest}."""
-    import bench
+def _decode_shard(rank, world, gpu, path):
+    """This rank's row groups of the one file at `path`: {(global rg, col): digest}."""
     import pqgpu
-    wl = bench.gen_workload("c5", _args(), rank, world)
-    pf, specs, (_, info) = wl.files[0]
-    rgs = info["row_groups"]
-    assert rgs == list(shard.row_groups_for_rank(8 * world, rank, world))
+    pf = pqgpu.ParquetFile.open(path)
+    rgs = list(shard.row_groups_for_rank(pf.num_row_groups, rank, world))
+    specs = [(rg, c) for rg in rgs for c in range(pf.num_columns)]
+    lo, hi, _ = pqgpu.chunk_span(pf, specs)
+    assert hi - lo < pf.size  # the other ranks' row groups are never read
     out = {}
     if gpu:
-        dec = pqgpu.GpuDecoder(0)
-        dev = dec.upload(pf.data)
+        fr = pqgpu.FileReader(path, decoder=pqgpu.GpuDecoder(0))
         try:
-            res = dec.decode_jobs([pqgpu.device_job(pf, rg, col, dev) for (rg, col) in specs])
-            for i, ((rg, col), r) in enumerate(zip(specs, res)):
-                d = dec.download(r, i)
-                out[(rgs[rg], col)] = _digest(d.status, d.num_slots, d.num_values,
-                                              (d.def_levels, d.rep_levels, d.values, d.offsets))
+            res = fr.decode_row_groups(rgs)
+            assert fr.uploaded_bytes == hi - lo
+            for i, (rg, col, r) in enumerate(res):
+                d = fr.dec.download(r, i)
+                out[(rg, col)] = _digest(d.status, d.num_slots, d.num_values,
+                                         (d.def_levels, d.rep_levels, d.values, d.offsets))
         finally:
-            dec.free(dev)
-            dec.close()
+            fr.dec.close()
     else:
         for (rg, col) in specs:
-            out[(rgs[rg], col)] = _oracle_digest(pf.host_job(rg, col)[0])
+            out[(rg, col)] = _oracle_digest(pf.host_job(rg, col)[0])
     return out
 
 
-def _worker(rank, world, port, q, gpu):
+def _worker(rank, world, port, q, gpu, path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -83,7 +84,7 @@ def _worker(rank, world, port, q, gpu):
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        mine = _decode_shard(rank, world, gpu)
+        mine = _decode_shard(rank, world, gpu, path)
         gathered = [None] * world
         dist.all_gather_object(gathered, mine)  # test-side merge only; bench.py has no data-path collective
         t = shard.max_elapsed(0.5 + rank, dist)
@@ -93,11 +94,20 @@ def _worker(rank, world, port, q, gpu):
         dist.destroy_process_group()
 
 
-def _run_two_ranks(gpu):
+def _one_file(tmp_path, world):
+    from gen import pqwrite as W
+    data, _ = W.config_c5(row_groups=range(8 * world), rows_per_rg=ROWS_PER_RG)
+    path = str(tmp_path / "c5_one_file.parquet")
+    with open(path, "wb") as f:
+        f.write(data)
+    return path
+
+
+def _run_two_ranks(gpu, path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, gpu)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, gpu, path)) for r in range(2)]
     for p in procs:
         p.start()
     gathered, t = q.get(timeout=240)
@@ -138,15 +148,51 @@ def test_partition_covers_all_row_groups():
         shard.row_groups_for_rank(4, 2, 2)
 
 
-def test_two_rank_gloo_shards_match_single_process():
-    gathered, t = _run_two_ranks(gpu=False)
+def test_two_rank_gloo_shards_match_single_process(tmp_path):
+    gathered, t = _run_two_ranks(False, _one_file(tmp_path, 2))
     assert t == 1.5  # MAX over ranks
     _check_merge(gathered, 2)
 
 
+def test_bench_rank_workload_is_the_one_files_row_groups():
+    """bench.py generates each rank's C5 row groups on the rank (the 64-row-group
+    file is ~52 GB): their chunk bytes equal those row groups' bytes in the one file."""
+    import bench
+    import pqgpu
+    from gen import pqwrite as W
+    one, _ = W.config_c5(row_groups=range(16), rows_per_rg=ROWS_PER_RG)
+    pone = pqgpu.ParquetFile(one)
+    wl = bench.gen_workload("c5", _args(), 1, 2)
+    pf, specs, (_, info) = wl.files[0]
+    assert info["row_groups"] == list(range(8, 16))
+    for (i, c) in specs:
+        a, b = pf.chunk_meta(i, c), pone.chunk_meta(8 + i, c)
+        assert (a.total_compressed_size, a.num_values) == (b.total_compressed_size, b.num_values)
+        assert bytes(pf.read_range(a.start, a.start + a.total_compressed_size)) == \
+            bytes(pone.read_range(b.start, b.start + b.total_compressed_size))
+
+
 @pytest.mark.gpu
-def test_two_rank_gpu_shards_match_single_process():
-    """Both ranks on cuda:0, each decoding its shard with libpqgpu."""
-    gathered, t = _run_two_ranks(gpu=True)
+def test_two_rank_gpu_shards_match_single_process(tmp_path):
+    """Both ranks on cuda:0, each range-reading its shard of the one file
+    through pqgpu.FileReader."""
+    gathered, t = _run_two_ranks(True, _one_file(tmp_path, 2))
     assert t == 1.5
     _check_merge(gathered, 2)
+
+
+@pytest.mark.gpu
+def test_bench_launches_ranks():
+    """`bench.py --gpus 2` with no launcher starts 2 ranks itself
+    (torch.distributed.run; here both on cuda:0 over gloo) and reports n_gpus 2."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--only", "c5",
+                          "--c5-rows-per-rg", "20000", "--steps", "2", "--warmup", "1", "--no-cpu"],
+                         capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["verified_bit_exact"]
