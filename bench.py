@@ -270,9 +270,9 @@ def cpu_baseline(wl, seconds):
 
 # ---------------------------------------------------------------- PMC traffic (committed passes)
 STAGE_KERNELS = {"scan": ["k_tile_jobs", "k_page_cands", "k_cand_parse", "k_tile_scan", "k_cand_link", "k_page_chain",
-                          "k_scan_pages"], "list": ["k_page_list"], "snappy": ["k_snappy"], "levels": ["k_page_levels"],
+                          "k_scan_pages"], "list": ["k_page_list"], "snappy": ["k_snap_plan", "k_snap_seg", "k_snap_link", "k_snap_decode", "k_snappy"], "levels": ["k_page_levels"],
                  "walk": ["k_hybrid_walk"], "unused": [], "nn_scan": ["k_nn_scan"],
-                 "values": ["k_values"], "strings": ["k_str_dict", "k_str_plain", "k_str_count", "k_char_scan",
+                 "values": ["k_values", "k_dict4"], "strings": ["k_str_dict", "k_str_plain", "k_str_count", "k_char_scan",
                                                   "k_str_copy"],
                  "finalize": ["k_finalize"]}
 
@@ -299,10 +299,10 @@ def run_workload(wl, dec, args, steps, warmup, barrier, dist, world, rank, cpu_s
     jobs = []
     wl.uploaded = 0
     for pf, specs, _ in wl.files:
-        # only the selected chunks' byte span goes to HBM (skipChunk, chunk_reader.go:286-312)
-        fj, dev, (lo, hi) = pqgpu.span_jobs(pf, specs, dec)
+        # only the selected chunks' bytes go to HBM (skipChunk, chunk_reader.go:286-312)
+        fj, dev, nbytes = pqgpu.span_jobs(pf, specs, dec)
         wl.devs.append(dev)
-        wl.uploaded += hi - lo
+        wl.uploaded += nbytes
         jobs += fj
     n = len(jobs)
     arr = (abi.ChunkJob * n)(*jobs)

@@ -134,6 +134,25 @@ constexpr int kHBlock = 512;      // values per expander block
 constexpr int kHBlockRuns = 64;   // runs per expander block (one per lane)
 constexpr int kHBlockBytes = 1008;  // payload bytes per block: 64 16-byte granules, aligned anywhere
 
+// One 4-byte dictionary data page, as the values kernel needs it (k_dict_plan).
+struct VRec {
+  uint8_t* out;            // values[:nn] of the page
+  const uint8_t* p;        // index stream (after the bit-width byte)
+  const RunEnt* runs;      // the stream's run table
+  const BlockDesc* blks;   // the stream's block index
+  const uint8_t* dict;     // dictionary entries (null: none)
+  int32_t n;               // stream bytes
+  int32_t w;               // index bit width (0: every key is 0)
+  int32_t nn;              // notNull
+  int32_t count;           // keys to expand: min(nn, the stream's produced)
+  int32_t n_blocks;
+  int32_t dcount;          // dictionary entries
+  int32_t job;             // -1: nothing to decode
+  int32_t pidx;            // PageDev index
+  int32_t serr;            // stream error met before nn keys (kOK: none)
+  int32_t produced;        // keys before that error
+};
+
 struct JobDev {
   // ---- inputs
   const uint8_t* data;

@@ -7,6 +7,7 @@
 // allocation or host synchronisation happens inside the enqueue once the
 // arenas have grown to the working-set size (capture-safe steady state).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include <algorithm>
 #include <cstdio>
@@ -59,6 +60,9 @@ __global__ void k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch);
 template <int Mode>
 __global__ void k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                          uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks);
+__global__ void k_dict_plan(JobDev* jobs, PageDev* pages, const int* list, const int* total, uint8_t* value_arena,
+                            const HStream* streams, const RunEnt* runs, const BlockDesc* blks, VRec* recs);
+__global__ void k_dict4(PageDev* pages, const int* total, int* queue, const VRec* recs);
 __global__ void k_finalize(JobDev* jobs, int n_jobs, PageDev* pages);
 __global__ void k_str_dict(JobDev* jobs, PageDev* pages, int64_t* doffs_arena);
 __global__ void k_str_count(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
@@ -76,6 +80,7 @@ int prof_read_values(unsigned long long* out);
 int prof_read_levels(unsigned long long* out);
 int prof_read_strings(unsigned long long* out);
 int prof_read_snappy(unsigned long long* out);
+int prof_read_dict(unsigned long long* out);
 }  // namespace pqg
 #endif
 
@@ -151,6 +156,10 @@ struct pqg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int num_cus = 256;
+  DevBuf vrecs;          // VRec per page-list entry (k_dict_plan -> k_dict4)
+  int dict4_per_cu = 2;  // resident k_dict4 workgroups per CU (LDS-bound), from the occupancy query
+  int dict4_threads = 256;
+  bool dict4 = true;     // k_dict4 for 4-byte dictionary pages (PQG_DICT4=0: k_values<1>, for A/B runs)
   int snappy_per_cu = 2;  // resident k_snappy waves per CU (LDS-bound: the output history ring)
   DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
   DevBuf tile_job;  // K1: tile -> job
@@ -222,6 +231,16 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
     return PQG_ERR_HIP;
   }
   for (auto& e : c->ev) hipEventCreate(&e);
+  if (const char* e = getenv("PQG_DICT4")) c->dict4 = atoi(e) != 0;
+  {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_dict4)) == hipSuccess && fa.maxThreadsPerBlock > 0)
+      c->dict4_threads = fa.maxThreadsPerBlock;  // kDWaves * 64 (pqg_dict.hip)
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, reinterpret_cast<const void*>(&k_dict4), c->dict4_threads, 0) ==
+            hipSuccess && o > 0)
+      c->dict4_per_cu = o;
+  }
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&k_snappy), 64, 0) ==
           hipSuccess &&
@@ -245,7 +264,7 @@ void pqg_ctx_destroy(pqg_ctx* c) {
                     &c->scratch, &c->streams, &c->runs, &c->blks, &c->cand_list, &c->vlists, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
                     &c->ok2slot, &c->order, &c->asm_seg, &c->offs_arena, &c->doffs_arena, &c->page_stage,
                     &c->blk_src, &c->blk_dst, &c->blk_meta, &c->tile_job, &c->sn_subs, &c->sn_segpage, &c->sn_F,
-                    &c->blk_subs, &c->blk_segpage, &c->blk_F})
+                    &c->blk_subs, &c->blk_segpage, &c->blk_F, &c->vrecs})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
   hipStreamDestroy(c->stream);
@@ -385,8 +404,10 @@ static int plan_batch(pqg_ctx* c) {
       c->succ.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->idx2slot.grow(sizeof(int) * (size_t)tile_total * kCandPerTile + 64) ||
       c->order.grow(sizeof(int) * (size_t)page_total + 64) ||
-      c->streams.grow(sizeof(HStream) * 3 * (size_t)page_total + 64) || c->runs.grow(sizeof(RunEnt) * (size_t)run_total + 64) ||
-      c->blks.grow(sizeof(BlockDesc) * (size_t)blk_total + 64) ||
+      c->streams.grow(sizeof(HStream) * 3 * (size_t)page_total + 64) ||
+      // slack past the last entry: k_dict4 stages run / descriptor granules past a stream's end
+      c->runs.grow(sizeof(RunEnt) * (size_t)run_total + 8192) || c->blks.grow(sizeof(BlockDesc) * (size_t)blk_total + 8192) ||
+      c->vrecs.grow(sizeof(VRec) * (size_t)std::max<int64_t>(page_total, 1)) ||
       c->offs_arena.grow(sizeof(int64_t) * (size_t)offs_total + 64) ||
       c->doffs_arena.grow(sizeof(int64_t) * (size_t)doffs_total + 64))
     return PQG_ERR_HIP;
@@ -491,8 +512,15 @@ static int launch_pipeline(pqg_ctx* c) {
   if (c->timed) hipEventRecord(c->ev[7], s);
   // every values kernel takes the whole page list and keeps the pages whose
   // vmode (set by k_page_levels) is its own
-  hipLaunchKernelGGL(k_values<1>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(3),
-                     (uint8_t*)c->value_arena.p, streams, runs, blks);
+  if (c->dict4) {  // 4-byte dictionary pages: pieces staged in LDS, small dictionaries in LDS (pqg_dict.hip)
+    VRec* recs = (VRec*)c->vrecs.p;
+    hipLaunchKernelGGL(k_dict_plan, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((c->list_cap + 255) / 256, c->num_cus * 4))),
+                       dim3(256), 0, s, jobs, pages, list, ctr, (uint8_t*)c->value_arena.p, streams, runs, blks, recs);
+    hipLaunchKernelGGL(k_dict4, dim3(qgrid(c->num_cus * c->dict4_per_cu)), dim3(c->dict4_threads), 0, s, pages, ctr, Q(3),
+                       recs);
+  } else
+    hipLaunchKernelGGL(k_values<1>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(3),
+                       (uint8_t*)c->value_arena.p, streams, runs, blks);
   if (c->any_fixed_other) {
     hipLaunchKernelGGL(k_values<0>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(2),
                        (uint8_t*)c->value_arena.p, streams, runs, blks);
@@ -811,19 +839,20 @@ int pqg_get_pages(pqg_ctx* c, int job, pqg_page_info* out, int cap) {
 }
 
 // Diagnostic builds (-DPQG_PROFILE): in-kernel phase cycle counters of the
-// values (slots 0-31), levels (slots 32-63), strings (64-95) and snappy
-// (96-127) translation units; read + reset.
+// values (slots 0-31), levels (slots 32-63), strings (64-95), snappy
+// (96-127) and dictionary (128-159) translation units; read + reset.
 int pqg_debug_counters(pqg_ctx* c, uint64_t* out, int cap) {
   if (!c || !out) return PQG_ERR_INVALID_ARG;
 #ifdef PQG_PROFILE
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
-  unsigned long long a[64], b[64], c3[64], d4[64];
+  unsigned long long a[64], b[64], c3[64], d4[64], e5[64];
   if (pqg::prof_read_values(a) || pqg::prof_read_levels(b) || pqg::prof_read_strings(c3) ||
-      pqg::prof_read_snappy(d4))
+      pqg::prof_read_snappy(d4) || pqg::prof_read_dict(e5))
     return PQG_ERR_HIP;
   int k = 0;
-  for (; k < 128 && k < cap; k++) out[k] = k < 32 ? a[k] : k < 64 ? b[k - 32] : k < 96 ? c3[k - 64] : d4[k - 96];
+  for (; k < 160 && k < cap; k++)
+    out[k] = k < 32 ? a[k] : k < 64 ? b[k - 32] : k < 96 ? c3[k - 64] : k < 128 ? d4[k - 96] : e5[k - 128];
   return k;
 #else
   return 0;

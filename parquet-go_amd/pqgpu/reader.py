@@ -293,14 +293,40 @@ def chunk_span(pf: ParquetFile, specs):
     return max(0, lo), min(hi, pf.size), metas
 
 
+def chunk_ranges(pf: ParquetFile, specs):
+    """The byte ranges the chunks of (rg, col) pairs occupy ([start, start +
+    TotalCompressedSize) each, clipped to the file), sorted, with overlapping or
+    adjacent ranges merged: [(lo, hi)], and the chunks' ChunkMetas."""
+    metas = [pf.chunk_meta(rg, c) for rg, c in specs]
+    rs = sorted((max(0, min(m.start, pf.size)), max(0, min(m.start + m.total_compressed_size, pf.size)))
+                for m in metas)
+    out = []
+    for lo, hi in rs:
+        if out and lo <= out[-1][1]:
+            out[-1][1] = max(out[-1][1], hi)
+        else:
+            out.append([lo, hi])
+    return [tuple(r) for r in out], metas
+
+
 def span_jobs(pf: ParquetFile, specs, dec):
-    """Chunk jobs for (rg, col) pairs with only their byte span uploaded to one
-    device buffer, each job pointing into it.  Unselected chunks are never
-    read, as skipChunk seeks past them (chunk_reader.go:286-312).  Returns
-    (jobs, device pointer of the span, (lo, hi))."""
-    lo, hi, metas = chunk_span(pf, specs)
-    span = np.ascontiguousarray(pf.read_range(lo, hi))
-    dev = dec.upload(span)
+    """Chunk jobs for (rg, col) pairs with only their chunks' bytes uploaded,
+    packed into one device buffer (merged ranges, chunk_ranges), each job
+    pointing into it.  Unselected chunks are never read, as skipChunk seeks past
+    them (chunk_reader.go:286-312).  A job's readable bytes run to the end of
+    its merged range, which holds all of [start, start + TotalCompressedSize)
+    that the file holds, so min(TotalCompressedSize, data_len) is what the
+    reference would read.  Returns (jobs, device pointer, bytes uploaded)."""
+    ranges, metas = chunk_ranges(pf, specs)
+    total = sum(hi - lo for lo, hi in ranges)
+    host = np.empty(max(total, 1), dtype=np.uint8)
+    base = []  # packed offset of each range
+    at = 0
+    for lo, hi in ranges:
+        host[at:at + hi - lo] = pf.read_range(lo, hi)
+        base.append(at)
+        at += hi - lo
+    dev = dec.upload(host)
     jobs = []
     for (rg, c), m in zip(specs, metas):
         job = abi.ChunkJob()
@@ -311,11 +337,13 @@ def span_jobs(pf: ParquetFile, specs, dec):
         job.num_values_hint = m.num_values
         job.total_uncompressed_size = m.total_uncompressed_size
         job.has_dict_page_offset = m.has_dict_page_offset
-        start = max(lo, min(m.start, lo + span.nbytes))
-        job.data = dev + (start - lo)
-        job.data_len = lo + span.nbytes - start  # readable bytes: to the span's end
+        start = max(0, min(m.start, pf.size))
+        k = max(i for i, (lo, _) in enumerate(ranges) if lo <= start)
+        lo, hi = ranges[k]
+        job.data = dev + base[k] + (start - lo)
+        job.data_len = hi - start
         jobs.append(job)
-    return jobs, dev, (lo, lo + span.nbytes)
+    return jobs, dev, total
 
 
 class FileReader:
@@ -355,8 +383,8 @@ class FileReader:
         specs = [(rg, c) for rg in rgs for c in self.selected]
         if not specs:
             return []
-        jobs, dev, (lo, hi) = span_jobs(self.file, specs, self.dec)
-        self.uploaded_bytes += hi - lo
+        jobs, dev, nbytes = span_jobs(self.file, specs, self.dec)
+        self.uploaded_bytes += nbytes
         try:
             res = self.dec.decode_jobs(jobs)
         finally:
@@ -368,8 +396,8 @@ class FileReader:
         specs = [(rg, c) for c in self.selected]
         if not specs:
             return {}
-        jobs, dev, (lo, hi) = span_jobs(self.file, specs, self.dec)
-        self.uploaded_bytes += hi - lo
+        jobs, dev, nbytes = span_jobs(self.file, specs, self.dec)
+        self.uploaded_bytes += nbytes
         try:
             res = self.dec.decode_jobs(jobs)
             return {self.file.columns[c].path.decode(): self.dec.download(r, i)

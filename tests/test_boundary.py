@@ -218,8 +218,10 @@ def test_file_reader_projection_uploads_selected_span(tmp_path):
             assert sorted(got) == ["i64d", "s"]
             for c in sel:
                 P.compare_chunk(P.oracle_chunk(pf, rg, c), got[pf.columns[c].path.decode()], "rg%d col%d" % (rg, c))
-        spans = [pqgpu.chunk_span(pf, [(rg, c) for c in sel]) for rg in range(2)]
-        assert fr.uploaded_bytes == sum(hi - lo for lo, hi, _ in spans) < len(data) // 2
+        ranges = [pqgpu.chunk_ranges(pf, [(rg, c) for c in sel])[0] for rg in range(2)]
+        want = sum(hi - lo for rs in ranges for lo, hi in rs)
+        metas = [pf.chunk_meta(rg, c) for rg in range(2) for c in sel]
+        assert fr.uploaded_bytes == want == sum(m.total_compressed_size for m in metas) < len(data) // 2
         lst = pqgpu.FileReader(str(path), "lst", decoder=dec)  # a group prefix selects its leaves
         assert [pf.columns[c].path.decode() for c in lst.selected] == ["lst.list.element"]
     finally:
