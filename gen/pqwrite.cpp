@@ -198,6 +198,33 @@ void dbp_encode(Buf& out, const T* v, int64_t n, int block = 128, int mbc = 4) {
   }
 }
 
+// DELTA_LENGTH_BYTE_ARRAY: DBP lengths, then the bytes (byteArrayDeltaLengthEncoder,
+// type_bytearray.go:142-187); DELTA_BYTE_ARRAY: DBP lengths of the prefix each
+// value shares with the previous one, then the suffixes as
+// DELTA_LENGTH_BYTE_ARRAY (byteArrayDeltaEncoder, type_bytearray.go:242-300).
+void delta_byte_array(Buf& out, const uint8_t* vals, const int64_t* offs, int64_t vs, int64_t ve, bool dba) {
+  const int64_t n = ve - vs;
+  std::vector<int32_t> lens, pre;
+  Buf chars;
+  const uint8_t* prev = nullptr;
+  int64_t plen = 0;
+  for (int64_t i = vs; i < ve; i++) {
+    const uint8_t* p = vals + offs[i];
+    const int64_t l = offs[i + 1] - offs[i];
+    int64_t k = 0;
+    if (dba)
+      while (k < l && k < plen && prev[k] == p[k]) k++;
+    pre.push_back((int32_t)k);
+    lens.push_back((int32_t)(l - k));
+    chars.insert(chars.end(), p + k, p + l);
+    prev = p;
+    plen = l;
+  }
+  if (dba) dbp_encode<int32_t>(out, pre.data(), n);
+  dbp_encode<int32_t>(out, lens.data(), n);
+  out.insert(out.end(), chars.begin(), chars.end());
+}
+
 // ---------------------------------------------------------------- snappy compressor
 void snappy_literal(Buf& o, const uint8_t* p, int64_t n) {
   while (n > 0) {
@@ -474,6 +501,8 @@ ChunkOut write_chunk(Buf& file, const ColSpec& c, int64_t s0, int64_t s1, int64_
       vals.push_back((uint8_t)idx_w);
       hybrid_encode(vals, idx.data() + (vs - v0), nn, idx_w, c.min_rle);
       any_dict = true;
+    } else if (enc == 6 || enc == 7) {
+      delta_byte_array(vals, c.values, c.offsets, vs, ve, enc == 7);
     } else if (enc == 5) {
       if (c.type == 1)
         dbp_encode<int32_t>(vals, (const int32_t*)c.values + vs, nn);
@@ -520,7 +549,7 @@ ChunkOut write_chunk(Buf& file, const ColSpec& c, int64_t s0, int64_t s1, int64_
   }
   if (any_dict) co.encodings.push_back(8);
   if (any_plain || c.encoding == 0) co.encodings.push_back(0);
-  if (c.encoding == 5) co.encodings.push_back(5);
+  if (c.encoding == 5 || c.encoding == 6 || c.encoding == 7) co.encodings.push_back(c.encoding);
   co.encodings.push_back(3);
   co.tcs = (int64_t)file.size() - co.start;
   co.num_values = s1 - s0;

@@ -13,6 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FLBA = range(8)
 PLAIN, RLE_DICTIONARY, DELTA_BINARY_PACKED = 0, 8, 5
+DELTA_LENGTH_BYTE_ARRAY, DELTA_BYTE_ARRAY = 6, 7
 UNCOMPRESSED, SNAPPY = 0, 1
 REQUIRED, OPTIONAL, LIST = 0, 1, 2
 
@@ -258,6 +259,34 @@ def config_c4(rows=50_000_000, vocab=65536, rows_per_page=20000, seed=4, dict_li
     col = Column("s", BYTE_ARRAY, out_chars, offsets=out_offs, encoding=RLE_DICTIONARY, codec=codec,
                  rows_per_page=rows_per_page, dict_limit=dict_limit)
     return write_file([col], rows), {"rows": rows, "chars": out_chars, "offsets": out_offs}
+
+
+def config_delta_strings(rows=200_000, encoding=DELTA_BYTE_ARRAY, rows_per_page=20000, seed=6, codec=SNAPPY,
+                         page_version=1, null_frac=0.0, sorted_values=True):
+    """STRING column written with DELTA_LENGTH_BYTE_ARRAY or DELTA_BYTE_ARRAY
+    (type_bytearray.go:98-240): values drawn from a vocabulary, sorted so that
+    neighbours share prefixes (the shape DELTA_BYTE_ARRAY is for), optional
+    nulls.  -> (file bytes, {"chars", "offsets", "defs"})."""
+    rng = np.random.default_rng(seed)
+    chars, offs = make_vocab(4096, seed)
+    words = [bytes(chars[offs[i]:offs[i + 1]]) for i in range(len(offs) - 1)]
+    prefixes = [b"http://example.com/", b"user_", b"", b"2024-01-"]
+    nn_rows = rows
+    defs = None
+    if null_frac > 0:
+        defs = (rng.random(rows) >= null_frac).astype(np.uint8)
+        nn_rows = int(defs.sum())
+    vals = [prefixes[int(rng.integers(0, len(prefixes)))] + words[int(rng.integers(0, len(words)))]
+            for _ in range(nn_rows)]
+    if sorted_values:
+        vals.sort()
+    out_offs = np.zeros(nn_rows + 1, dtype=np.int64)
+    out_offs[1:] = np.cumsum([len(v) for v in vals])
+    out_chars = np.frombuffer(b"".join(vals), dtype=np.uint8).copy() if vals else np.zeros(0, np.uint8)
+    col = Column("s", BYTE_ARRAY, out_chars, offsets=out_offs, encoding=encoding, codec=codec,
+                 rows_per_page=rows_per_page, page_version=page_version,
+                 repetition=OPTIONAL if defs is not None else REQUIRED, def_levels=defs)
+    return write_file([col], rows), {"chars": out_chars, "offsets": out_offs, "defs": defs}
 
 
 def config_c2_family(rows=100_000_000, bits_list=(1, 2, 4, 8, 12, 16, 20), null_frac=0.10, rows_per_page=20000,

@@ -75,6 +75,9 @@ struct PageDev {
   // and their offset in the chunk's chars (exclusive scan over the pages)
   int64_t chars;
   int64_t char_offset;
+  // DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY: where the value bytes (the
+  // suffixes) start in the values section, after the DBP length stream(s)
+  int64_t cstart;
   // K2 snappy split (pqg_snappy.hip, k_snap_plan): bytes of the block's
   // length varint, 64 KiB output sub-blocks and their SnapSub entries, 4 KiB
   // compressed segments, and the serial-fallback flag (non-zero: k_snappy
@@ -211,7 +214,10 @@ constexpr int kQueueInts = kQShards * kQStride;
 constexpr int kModePresentOff = 1024 + 9 * kQueueInts;
 // the serial snappy pass (k_snappy after the split decode) pulls its own queue
 constexpr int kQueueSnapSerial = 10;
-constexpr int kQueueSlots = 11;  // queue regions zeroed per launch: 0-8, the stage flags (9), 10
+// DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY lengths (k_str_delta) and values (k_str_dba)
+constexpr int kQueueStrDelta = 11;
+constexpr int kQueueStrDba = 12;
+constexpr int kQueueSlots = 13;  // queue regions zeroed per launch: 0-8, the stage flags (9), 10-12
 
 // Scan tiles of the speculative page-header search.
 constexpr int kScanTile = 16384;

@@ -58,11 +58,11 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
 __device__ __forceinline__ int bits_len(uint32_t v) { return v ? 32 - __builtin_clz(v) : 0; }
 
-// getValuesDecoder chunk_reader.go:143-196 (DELTA_*_BYTE_ARRAY are outside this build)
+// getValuesDecoder chunk_reader.go:143-196 (DELTA_BYTE_ARRAY on FIXED_LEN_BYTE_ARRAY is outside this build)
 __device__ __forceinline__ int values_supported(int type, int type_length, int enc) {
   switch (type) {
     case 0: return enc == 0 || enc == 3 || enc == 8;
-    case 6: return enc == 0 || enc == 8;
+    case 6: return enc == 0 || enc == 8 || enc == 6 || enc == 7;  // + DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY
     case 7: return type_length >= 0 && (enc == 0 || enc == 8);
     case 3: case 4: case 5: return enc == 0 || enc == 8;
     case 1: case 2: return enc == 0 || enc == 5 || enc == 8;
@@ -394,5 +394,44 @@ struct Window {
     return lds[i - base];
   }
 };
+
+// ---- varints of DELTA_BINARY_PACKED headers (helpers.go:149-183 via
+// binary.ReadUvarint / ReadVarint), through a Window, with the oracle's error
+// classes
+__device__ __forceinline__ int read_uvarint64(Window& w, int64_t& pos, uint64_t* out) {
+  uint64_t x = 0;
+  unsigned s = 0;
+  for (int i = 0;; i++) {
+    int b = w.get(pos);
+    if (b < 0) return kEOF;
+    pos++;
+    if (b < 0x80) {
+      if (i > 9 || (i == 9 && b > 1)) return kRLE;
+      *out = x | (s < 64 ? (uint64_t)b << s : 0);
+      return kOK;
+    }
+    if (s < 64) x |= (uint64_t)(b & 0x7f) << s;
+    s += 7;
+  }
+}
+// readVariant32 / readVariant64 with the oracle's error classes
+__device__ __forceinline__ int read_signed(Window& w, int64_t& pos, bool is64, uint64_t* out) {
+  uint64_t ux;
+  int e = read_uvarint64(w, pos, &ux);
+  if (e) return e == kEOF ? kEOF : kDELTA;
+  int64_t x = (int64_t)(ux >> 1);
+  if (ux & 1) x = ~x;
+  if (!is64 && (x > 2147483647LL || x < -2147483648LL)) return kDELTA;
+  *out = (uint64_t)x;
+  return kOK;
+}
+__device__ __forceinline__ int read_u32var_delta(Window& w, int64_t& pos, int32_t* out) {
+  uint64_t v;
+  int e = read_uvarint64(w, pos, &v);
+  if (e) return e == kEOF ? kEOF : kDELTA;
+  if (v > 0x7fffffffull) return kDELTA;
+  *out = (int32_t)v;
+  return kOK;
+}
 
 }  // namespace pqg

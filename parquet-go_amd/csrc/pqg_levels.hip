@@ -944,6 +944,8 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
       P.vmode = vm;
       int* present = const_cast<int*>(total) + kModePresentOff;
       if (present[vm] == 0) present[vm] = 1;
+      // flag 4: DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY pages (k_str_delta, k_str_dba)
+      if (vm == 2 && (pg.encoding == 6 || pg.encoding == 7) && present[4] == 0) present[4] = 1;
     }
     // ---- readValues (page_v1.go:27-55): rep levels, then def levels
     int64_t nn = 0;

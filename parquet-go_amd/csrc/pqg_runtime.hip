@@ -70,6 +70,10 @@ __global__ void k_str_count(JobDev* jobs, PageDev* pages, const int* list, const
 __global__ void k_str_plain(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                             int64_t* offs_arena);
 __global__ void k_char_scan(JobDev* jobs, PageDev* pages, int64_t* offs_arena);
+__global__ void k_str_delta(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                            int64_t* offs_arena);
+__global__ void k_str_dba(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                          uint8_t* value_arena, int64_t* offs_arena);
 __global__ void k_str_copy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                            uint8_t* value_arena, int64_t* offs_arena);
 }  // namespace pqg
@@ -534,9 +538,13 @@ static int launch_pipeline(pqg_ctx* c) {
     hipLaunchKernelGGL(k_str_plain, dim3(qgrid(c->num_cus * 4)), dim3(512), 0, s, jobs, pages, list, ctr, Q(5), offs);
     hipLaunchKernelGGL(k_str_count, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(4), offs, streams, runs,
                        blks);
+    hipLaunchKernelGGL(k_str_delta, dim3(qgrid(c->num_cus * 8)), dim3(64), 0, s, jobs, pages, list, ctr,
+                       Q(kQueueStrDelta), offs);
     hipLaunchKernelGGL(k_char_scan, dim3(n), dim3(256), 0, s, jobs, pages, offs);
     hipLaunchKernelGGL(k_str_copy, dim3(qgrid(c->num_cus * 4)), dim3(512), 0, s, jobs, pages, list, ctr, Q(6),
                        (uint8_t*)c->value_arena.p, offs);
+    hipLaunchKernelGGL(k_str_dba, dim3(qgrid(c->num_cus * 6)), dim3(64), 0, s, jobs, pages, list, ctr,
+                       Q(kQueueStrDba), (uint8_t*)c->value_arena.p, offs);
   }
   if (c->timed) hipEventRecord(c->ev[9], s);
   hipLaunchKernelGGL(k_finalize, dim3(n), dim3(256), 0, s, jobs, n, pages);

@@ -435,6 +435,8 @@ __global__ void __launch_bounds__(64) k_str_count(JobDev* jobs, PageDev* pages, 
         if (bad < nn && (serr == kOK || bad < S.produced)) de = kDICT_INDEX;
         else de = serr;
       }
+    } else if (enc == 6 || enc == 7) {
+      continue;  // DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY: k_str_delta
     } else {
       de = kUNSUPPORTED;
     }
@@ -442,6 +444,362 @@ __global__ void __launch_bounds__(64) k_str_count(JobDev* jobs, PageDev* pages, 
       PageDev& o = pages[pidx];
       o.chars = chars;
       if (de != kOK) o.decode_status = de;
+    }
+  }
+}
+
+// ---- K7e: DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY lengths -------------------
+// deltaBitPackDecoder32 (deltabp_decoder.go:38-175) walked exactly as
+// decodeInt32 (helpers.go:119-129) drives it from byteArrayDeltaLengthDecoder /
+// byteArrayDeltaDecoder.init (type_bytearray.go:103-111, 194-212): every one of
+// the header's valuesCount values, 8 at a time (a group is read when position %
+// 8 == 0, a miniblock header when a block's miniblocks are used up; the last
+// group skips the rest of the block with the sic width of miniBlockBitWidth
+// [currentMiniBlock]).  The stream is read through an LDS window; lanes 0..7
+// unpack a group's 8 deltas, and a DPP prefix sum turns them into values.
+struct DbpWalk32 {
+  Window win;
+  int64_t r;           // reader position (stream offset)
+  int32_t bs, mbc, total, mbvc;
+  int32_t prev, mind;
+  int64_t wpos;        // stream offset of the current block's width bytes
+  int32_t cur, mbpos, cw;
+  int32_t position;
+
+  __device__ int init(gcu8 p, int64_t n, PQG_L uint8_t* lds, int64_t start) {
+    win = Window{p, n, kFarAway, lds};
+    r = start;
+    int e;
+    uint64_t first;
+    if ((e = read_u32var_delta(win, r, &bs))) return e;
+    if (bs <= 0 && bs % 128 != 0) return kDELTA;
+    if ((e = read_u32var_delta(win, r, &mbc))) return e;
+    if (mbc <= 0 || bs % mbc != 0) return kDELTA;
+    mbvc = bs / mbc;
+    if (mbvc == 0) return kDELTA;
+    if ((e = read_u32var_delta(win, r, &total))) return e;
+    if ((e = read_signed(win, r, false, &first))) return e;
+    prev = (int32_t)first;
+    position = 0;
+    return mini_header();
+  }
+  // readMiniBlockHeader :89-112
+  __device__ int mini_header() {
+    uint64_t md;
+    int e = read_signed(win, r, false, &md);
+    if (e) return e;
+    mind = (int32_t)md;
+    if (win.n - r < mbc) {  // io.ReadFull of the widths
+      r = win.n;
+      return kEOF;
+    }
+    wpos = r;
+    for (int32_t m = 0; m < mbc; m++)
+      if (win.get(r + m) > 32) return kBIT_WIDTH;
+    r += mbc;
+    cur = 0;
+    return kOK;
+  }
+  // next() for positions [position, position + 8) (those < total): lane j < 8
+  // gets the value of position + j in *v.  kOK or the error of the group.
+  __device__ int group(int32_t* v) {
+    const int lane = lane_id();
+    if (position % mbvc == 0) {
+      if (cur >= mbc) {
+        const int e = mini_header();
+        if (e) return e;
+      }
+      cw = win.get(wpos + cur);
+      mbpos = 0;
+      cur++;
+    }
+    if (win.n - r < cw) {  // io.ReadFull of the group
+      r = win.n;
+      return kEOF;
+    }
+    // the group's bytes into the window, then lane j < 8 unpacks delta j
+    if (cw > 0 && (r < win.base || r + cw > win.base + kWin)) win.fill(r);
+    uint32_t d = 0;
+    if (cw > 0 && lane < 8) {
+      const int64_t b0 = (int64_t)lane * cw;  // bit of delta j in the group
+      const PQG_L uint8_t* g = win.lds + (r - win.base);
+      uint64_t x = 0;
+      for (int k = 0; k < 5; k++) {
+        const int64_t by = (b0 >> 3) + k;
+        if (by < cw) x |= (uint64_t)g[by] << (8 * k);
+      }
+      x >>= (b0 & 7);
+      d = (uint32_t)(cw == 32 ? x : (x & ((1ull << cw) - 1)));
+    }
+    r += cw;
+    mbpos += cw;
+    if ((int64_t)position + 8 >= total) {
+      const int64_t l = (int64_t)(mbvc / 8) * cw - mbpos;
+      if (l < 0) return kDELTA;  // "invalid stream"
+      r = r + l < win.n ? r + l : win.n;  // errors ignored
+      if (cur < mbc) {
+        const int w2 = win.get(wpos + cur);  // sic: miniBlockBitWidth[currentMiniBlock]
+        if (w2 != 0) {
+          const int64_t skip = (int64_t)(mbc - cur) * (int64_t)(mbvc / 8) * w2;
+          r = r + skip < win.n ? r + skip : win.n;
+        }
+      }
+    }
+    // value(position + j) = prev + sum_{k < j} (delta_k + mind), int32 wrapping
+    const uint32_t step = (lane < 8) ? d + (uint32_t)mind : 0u;
+    uint32_t incl = step;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if ((lane & 7) >= o) incl += t;
+    }
+    *v = (int32_t)((uint32_t)prev + incl - step);
+    prev = (int32_t)((uint32_t)prev + (uint32_t)__shfl(incl, 7, 64));
+    position += 8;
+    return kOK;
+  }
+};
+
+// One wave per DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY page: the read phase
+// (every length decoded, the prefix/suffix count check) and the lengths of the
+// page's notNull values: page-relative value ends (DLBA) or, for
+// DELTA_BYTE_ARRAY, prefix << 32 | suffix end, in the chunk's offsets (K7f /
+// k_str_copy turn them into chunk offsets); page.chars, page.cstart.  The
+// first failing value, in order, is the page's decode error
+// (byteArrayDeltaLengthDecoder.next :113-126; byteArrayDeltaDecoder
+// .decodeValues :214-240).
+struct DeltaStrShared {
+  uint8_t win[2][kWin];
+};
+__global__ void __launch_bounds__(64) k_str_delta(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+                                                  int* queue, int64_t* offs_arena) {
+  __shared__ __attribute__((aligned(16))) DeltaStrShared sh;
+  const int lane = lane_id();
+  if (total[kModePresentOff + 4] == 0) return;  // no DELTA_*_BYTE_ARRAY page
+  for (;;) {
+    const int t = queue_next(queue);
+    if (t >= *total) return;
+    const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
+    const PageDev pg = pages[pidx];
+    if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3) || pg.vmode != 2 ||
+        (pg.encoding != 6 && pg.encoding != 7))
+      continue;
+    const JobDev job = jobs[pg.job];
+    if (job.status == kCAPACITY) continue;
+    const bool dba = pg.encoding == 7;
+    const gcu8 val = gconst(pg.val);
+    const int64_t vn = pg.val_n;
+    const int64_t nn = pg.decode_status == kOK ? pg.not_null : 0;
+    // ---- read phase: lengths (DBA: prefixes, then suffix lengths)
+    DbpWalk32 A, B;  // A: prefix lengths (DBA) / lengths; B: suffix lengths (DBA)
+    // a length count beyond the page's NumValues is refused (the oracle's
+    // DeltaLength::init: unbounded work for zero-width miniblocks otherwise)
+    int re = A.init(val, vn, lds_ptr(sh.win[0]), 0);
+    if (re == kOK && A.total > pg.num_values) re = kDELTA;
+    int64_t a_end = 0;
+    if (re == kOK) {
+      for (int32_t p = 0; p < A.total && re == kOK; p += 8) {
+        int32_t v;
+        re = A.group(&v);
+      }
+      a_end = A.r;
+    }
+    if (re == kOK && dba) {
+      re = B.init(val, vn, lds_ptr(sh.win[1]), a_end);
+      if (re == kOK && B.total > pg.num_values) re = kDELTA;
+      if (re == kOK) {
+        for (int32_t p = 0; p < B.total && re == kOK; p += 8) {
+          int32_t v;
+          re = B.group(&v);
+        }
+      }
+      if (re == kOK && A.total != B.total) re = kDELTA;  // "different number of suffixes and prefixes"
+    }
+    if (re != kOK) {
+      if (lane == 0) pages[pidx].read_status = re;
+      continue;
+    }
+    if (nn == 0) continue;
+    // ---- decodeValues over the notNull values: walk the length stream(s)
+    // again, 8 values at a time, checking each value in order
+    const int64_t cs = dba ? B.r : A.r;  // the value bytes start where the lengths end
+    const int32_t cnt = dba ? B.total : A.total;
+    PQG_G int64_t* slots = gmut(offs_arena) + job.offs_base + pg.value_offset + 1;
+    int e = A.init(val, vn, lds_ptr(sh.win[0]), 0);
+    if (dba) e = B.init(val, vn, lds_ptr(sh.win[1]), a_end);
+    (void)e;
+    int64_t bad = INT64_MAX;  // first failing value
+    int bad_e = kOK;
+    int64_t send = 0;         // suffix / value bytes so far
+    int64_t chars = 0;        // output bytes so far
+    int64_t prevlen = 0;      // DBA: length of the previous value
+    for (int64_t i0 = 0; i0 < nn; i0 += 8) {
+      if (i0 >= cnt) {  // next(): position >= len(lens) -> io.EOF
+        if (i0 < bad) { bad = i0; bad_e = kEOF; }
+        break;
+      }
+      int32_t pl = 0, sl = 0;
+      if (dba) {
+        A.group(&pl);
+        B.group(&sl);
+      } else {
+        A.group(&sl);
+      }
+      const int64_t i = i0 + lane;
+      const bool live = lane < 8 && i < nn;
+      // per value, in the reference's order: position, negative length, short
+      // read, (DBA) capacity, previous-value length
+      int ve = kOK;
+      int64_t my_send = 0, my_len = 0;
+      {
+        const int64_t s64 = (live && i < cnt && sl > 0) ? sl : 0;
+        int64_t incl = s64;
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+          const int64_t tt = __shfl_up(incl, o, 64);
+          if ((lane & 7) >= o) incl += tt;
+        }
+        my_send = send + incl;
+        const int64_t eff_pl = dba && pl > 0 ? pl : 0;
+        my_len = eff_pl + s64;
+        int64_t li = my_len;
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+          const int64_t tt = __shfl_up(li, o, 64);
+          if ((lane & 7) >= o) li += tt;
+        }
+        int64_t prev_l = __shfl_up(my_len, 1, 64);
+        if (lane == 0) prev_l = prevlen;
+        if (live) {
+          if (i >= cnt) ve = kEOF;
+          else if (sl < 0) ve = kBYTE_ARRAY;                     // make([]byte, negative)
+          else if (cs + my_send > vn) ve = kEOF;                 // io.ReadFull: "there is no byte left"
+          else if (dba && (int64_t)pl + sl < 0) ve = kBYTE_ARRAY; // negative capacity
+          else if (dba && prev_l < (int64_t)pl) ve = kBYTE_ARRAY; // "invalid prefix len in the stream"
+        }
+        if (live && ve == kOK)
+          slots[i] = dba ? (int64_t)(((uint64_t)eff_pl << 32) | (uint64_t)(uint32_t)my_send) : my_send;
+        const int64_t tot_s = __shfl(incl, 7, 64), tot_l = __shfl(li, 7, 64);
+        send += tot_s;
+        chars += tot_l;
+        prevlen = __shfl(my_len, 7, 64);
+      }
+      const uint64_t eb = __ballot(ve != kOK);
+      if (eb) {
+        const int l = __ffsll((long long)eb) - 1;
+        bad = i0 + l;
+        bad_e = __builtin_amdgcn_readlane(ve, l);
+        break;
+      }
+    }
+    if (lane == 0) {
+      PageDev& o = pages[pidx];
+      o.cstart = cs;
+      o.chars = bad_e == kOK ? chars : 0;
+      if (bad_e != kOK) o.decode_status = bad_e;
+    }
+  }
+}
+
+// ---- K7f: DELTA_BYTE_ARRAY values ----------------------------------------------
+// value i = value(i - 1)[:prefix_i] + suffix_i (type_bytearray.go:214-240): one
+// wave per page, values in order.  The previous value stays in LDS (values up
+// to kDbaPrev bytes; a longer one is rebuilt from the output it was written
+// to), each group's 64 suffixes are staged into LDS with one round of loads,
+// and each value is assembled in LDS and stored, 64 bytes per lane step.
+constexpr int kDbaPrev = 16384;
+constexpr int kDbaStage = 8192;
+struct DbaShared {
+  uint8_t prev[kDbaPrev];
+  uint8_t stage[kDbaStage + 64];
+};
+__global__ void __launch_bounds__(64) k_str_dba(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+                                                int* queue, uint8_t* value_arena, int64_t* offs_arena) {
+  __shared__ __attribute__((aligned(16))) DbaShared sh;
+  const int lane = lane_id();
+  if (total[kModePresentOff + 4] == 0) return;
+  for (;;) {
+    const int t = queue_next(queue);
+    if (t >= *total) return;
+    const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
+    const PageDev pg = pages[pidx];
+    if (pg.read_status != kOK || pg.decode_status != kOK || (pg.page_type != 0 && pg.page_type != 3) ||
+        pg.vmode != 2 || pg.encoding != 7 || pg.not_null == 0)
+      continue;
+    const JobDev job = jobs[pg.job];
+    if (job.status == kCAPACITY) continue;
+    const int64_t nn = pg.not_null, base = pg.char_offset;
+    const gu8 chars = gmut(value_arena) + job.value_base + base;
+    PQG_G int64_t* slots = gmut(offs_arena) + job.offs_base + pg.value_offset + 1;
+    const gcu8 suf = gconst(pg.val) + pg.cstart;
+    int64_t oend = 0, sprev = 0;  // output end, suffix start of the next value
+    int64_t plen = 0;             // length of the previous value
+    bool in_lds = true;           // the previous value is in sh.prev
+    int64_t pstart = 0;           // its output offset (page-relative)
+    for (int64_t i0 = 0; i0 < nn; i0 += 64) {
+      const int64_t i = i0 + lane;
+      int64_t pl = 0, se = sprev;
+      if (i < nn) {
+        const uint64_t x = (uint64_t)slots[i];
+        pl = (int64_t)(x >> 32);
+        se = (int64_t)(uint32_t)x;
+      }
+      int64_t ss = __shfl_up(se, 1, 64);
+      if (lane == 0) ss = sprev;
+      const int64_t len = i < nn ? pl + (se - ss) : 0;
+      int64_t incl;
+      const int64_t ex = wave_excl_scan_i64(len, &incl);
+      const int64_t ostart = oend + ex;
+      if (i < nn) slots[i] = base + ostart + len;
+      const int nv = (int)(nn - i0 < 64 ? nn - i0 : 64);
+      const int64_t g_ss = sprev, g_se = __shfl(se, nv - 1, 64);
+      // the group's suffixes into LDS (when they fit)
+      const bool staged = g_se - g_ss <= kDbaStage;
+      if (staged)
+        for (int64_t b = lane; b < g_se - g_ss; b += 64) sh.stage[b] = suf[g_ss + b];
+      __builtin_amdgcn_wave_barrier();
+      for (int k = 0; k < nv; k++) {
+        const int64_t kpl = __shfl(pl, k, 64), kss = __shfl(ss, k, 64), kse = __shfl(se, k, 64);
+        const int64_t klen = __shfl(len, k, 64), kost = __shfl(ostart, k, 64);
+        const int64_t ksl = kse - kss;
+        if (klen <= kDbaPrev) {
+          if (!in_lds && kpl > 0) {
+            // the previous value was too long for LDS: its prefix from the output
+            __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): this wave's stores of it are done
+            for (int64_t b = lane; b < kpl; b += 64)
+              sh.prev[b] = (uint8_t)(ld_l2_u32((const PQG_G uint32_t*)((uintptr_t)(chars + pstart + b) & ~(uintptr_t)3)) >>
+                                     (8 * ((uintptr_t)(chars + pstart + b) & 3)));
+            __builtin_amdgcn_wave_barrier();
+          }
+          for (int64_t b = lane; b < ksl; b += 64)
+            sh.prev[kpl + b] = staged ? sh.stage[kss - g_ss + b] : suf[kss + b];
+          __builtin_amdgcn_wave_barrier();
+          for (int64_t b = lane; b < klen; b += 64) chars[kost + b] = sh.prev[b];
+          __builtin_amdgcn_wave_barrier();
+          in_lds = true;
+        } else {
+          // a value longer than the LDS buffer: prefix from the previous value's
+          // output (LDS or memory), suffix from the page
+          __builtin_amdgcn_s_waitcnt(0);
+          for (int64_t b = lane; b < kpl; b += 64) {
+            uint8_t c;
+            if (in_lds) c = sh.prev[b];
+            else {
+              const uintptr_t a = (uintptr_t)(chars + pstart + b);
+              c = (uint8_t)(ld_l2_u32((const PQG_G uint32_t*)(a & ~(uintptr_t)3)) >> (8 * (a & 3)));
+            }
+            chars[kost + b] = c;
+          }
+          for (int64_t b = lane; b < ksl; b += 64) chars[kost + kpl + b] = suf[kss + b];
+          in_lds = false;
+        }
+        plen = klen;
+        pstart = kost;
+      }
+      (void)plen;
+      oend += incl;
+      sprev = g_se;
+      __builtin_amdgcn_wave_barrier();
     }
   }
 }
@@ -501,11 +859,12 @@ __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, 
     const int pidx = list[t];
     const PageDev& pg = pages[pidx];
     if (pg.read_status != kOK || pg.decode_status != kOK || (pg.page_type != 0 && pg.page_type != 3) || pg.vmode != 2 ||
-        pg.not_null == 0)
+        pg.not_null == 0 || pg.encoding == 7)  // DELTA_BYTE_ARRAY: k_str_dba
       continue;
     const JobDev& job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
     const int64_t nn = pg.not_null, base = pg.char_offset;
+    const bool dlba = pg.encoding == 6;  // value bytes back to back from cstart
     const gu8 chars = gmut(value_arena) + job.value_base + base;
     PQG_G int64_t* ends = gmut(offs_arena) + job.offs_base + pg.value_offset + 1;
     const bool dict = pg.encoding == 8;
@@ -530,7 +889,7 @@ __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, 
         if (i < nn) {
           e = ends[i];
           s0 = threadIdx.x ? ends[i - 1] : s_prev;
-          from = s0 + 4 * (i + 1);
+          from = dlba ? pg.cstart + s0 : s0 + 4 * (i + 1);
         }
         __syncthreads();  // every end of the round is read before any is rewritten
         if (i == (i0 + 512 < nn ? i0 + 511 : nn - 1)) s_prev = e;

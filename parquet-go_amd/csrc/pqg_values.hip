@@ -184,42 +184,6 @@ struct DbpShared {
   uint64_t gvals[8];                    // generic path: current 8-group
 };
 
-__device__ __forceinline__ int read_uvarint64(Window& w, int64_t& pos, uint64_t* out) {
-  uint64_t x = 0;
-  unsigned s = 0;
-  for (int i = 0;; i++) {
-    int b = w.get(pos);
-    if (b < 0) return kEOF;
-    pos++;
-    if (b < 0x80) {
-      if (i > 9 || (i == 9 && b > 1)) return kRLE;
-      *out = x | (s < 64 ? (uint64_t)b << s : 0);
-      return kOK;
-    }
-    if (s < 64) x |= (uint64_t)(b & 0x7f) << s;
-    s += 7;
-  }
-}
-// readVariant32 / readVariant64 with the oracle's error classes
-__device__ __forceinline__ int read_signed(Window& w, int64_t& pos, bool is64, uint64_t* out) {
-  uint64_t ux;
-  int e = read_uvarint64(w, pos, &ux);
-  if (e) return e == kEOF ? kEOF : kDELTA;
-  int64_t x = (int64_t)(ux >> 1);
-  if (ux & 1) x = ~x;
-  if (!is64 && (x > 2147483647LL || x < -2147483648LL)) return kDELTA;
-  *out = (uint64_t)x;
-  return kOK;
-}
-__device__ __forceinline__ int read_u32var_delta(Window& w, int64_t& pos, int32_t* out) {
-  uint64_t v;
-  int e = read_uvarint64(w, pos, &v);
-  if (e) return e == kEOF ? kEOF : kDELTA;
-  if (v > 0x7fffffffull) return kDELTA;
-  *out = (int32_t)v;
-  return kOK;
-}
-
 // Values of a DBP page: emulates deltaBitPackDecoder{32,64}.next for positions
 // [0, nn).  Regular layout (miniblock value count a multiple of 8, <= kMaxMb
 // miniblocks): wave-parallel unpack + wrapping scan; otherwise one lane.

@@ -1,0 +1,217 @@
+"""DELTA_LENGTH_BYTE_ARRAY and DELTA_BYTE_ARRAY: the oracle's
+restatement of byteArrayDeltaLengthDecoder / byteArrayDeltaDecoder
+(type_bytearray.go:97-240, lengths through deltaBitPackDecoder32
+deltabp_decoder.go:38-175) against the generator's own values and against
+pyarrow (an independent writer and reader), the error classes of hand-built
+pages, and (-m gpu) the GPU path (k_str_delta, k_str_copy, k_str_dba) against
+the oracle on the same files, byte for byte.
+
+The reference's own tests hold no vectors for these encodings (types_test.go
+:189-214 only round-trips 2000 random values through its encoder): parity is
+pinned by the format, by pyarrow, and by the quirks of the cited lines
+(Q3: a one-value length stream has no miniblock, so init fails with EOF)."""
+import io
+
+import numpy as np
+import pytest
+
+import parity as P
+import pqtest_util as U
+from gen import pqwrite as W
+from oracle import pyoracle as O
+from pqgpu import abi
+
+DLBA, DBA = W.DELTA_LENGTH_BYTE_ARRAY, W.DELTA_BYTE_ARRAY
+
+
+def _strings(r):
+    offs = np.asarray(r.offsets)
+    v = np.asarray(r.values)
+    return [bytes(v[offs[i]:offs[i + 1]]) for i in range(len(offs) - 1)]
+
+
+def _expected(exp):
+    offs, chars = exp["offsets"], exp["chars"]
+    return [bytes(chars[offs[i]:offs[i + 1]]) for i in range(len(offs) - 1)]
+
+
+CASES = [dict(encoding=e, page_version=v, codec=c, null_frac=nf, sorted_values=s)
+         for e in (DLBA, DBA) for v in (1, 2) for c in (W.UNCOMPRESSED, W.SNAPPY)
+         for nf, s in ((0.0, True), (0.15, False))]
+
+
+@pytest.mark.parametrize("kw", CASES, ids=lambda k: "e%d_v%d_c%d_n%d_s%d" % (
+    k["encoding"], k["page_version"], k["codec"], int(k["null_frac"] * 100), k["sorted_values"]))
+def test_oracle_generated_files(kw):
+    import pqgpu
+    data, exp = W.config_delta_strings(rows=12000, rows_per_page=2500, **kw)
+    pf = pqgpu.ParquetFile(data)
+    r = O.decode_chunk(pf.host_job(0, 0)[0])
+    assert r.status == 0, abi.status_name(r.status)
+    assert _strings(r) == _expected(exp)
+    if exp["defs"] is not None:
+        assert np.array_equal(np.asarray(r.def_levels), exp["defs"])
+
+
+@pytest.mark.parametrize("enc", ["DELTA_LENGTH_BYTE_ARRAY", "DELTA_BYTE_ARRAY"])
+@pytest.mark.parametrize("version", ["1.0", "2.0"])
+def test_oracle_pyarrow_files(enc, version):
+    """pyarrow's writer and reader (independent of the generator and of the
+    reference) agree with the oracle."""
+    pa = pytest.importorskip("pyarrow")
+    pq = pytest.importorskip("pyarrow.parquet")
+    import pqgpu
+    rng = np.random.default_rng(11)
+    words = sorted("w%05d_%s" % (i, "xyz" * int(rng.integers(0, 9))) for i in range(2000))
+    arr = pa.array([words[int(i)] if rng.random() > 0.1 else None for i in rng.integers(0, 2000, 9000)])
+    buf = io.BytesIO()
+    pq.write_table(pa.table({"s": arr}), buf, use_dictionary=False, column_encoding={"s": enc},
+                   data_page_version=version, compression="snappy", data_page_size=20000)
+    pf = pqgpu.ParquetFile(buf.getvalue())
+    r = O.decode_chunk(pf.host_job(0, 0)[0])
+    assert r.status == 0, abi.status_name(r.status)
+    assert _strings(r) == [x.encode() for x in arr.to_pylist() if x is not None]
+
+
+# ---------------------------------------------------------------- hand-built pages
+def _dlba(lens, chars):
+    return W.dbp_encode(np.asarray(lens, dtype=np.int32), bits=32) + bytes(chars)
+
+
+def _dba(prefix, suffix_lens, chars):
+    return W.dbp_encode(np.asarray(prefix, dtype=np.int32), bits=32) + _dlba(suffix_lens, chars)
+
+
+def _page_chunk(values_section, nvals, enc):
+    return U.v1_page(values_section, nvals, enc)
+
+
+def hand_cases():
+    """(name, chunk bytes, expected oracle status) — statuses follow the cited lines."""
+    ok_lens = [3, 0, 5, 2, 7, 1, 4, 4, 2]
+    chars = bytes(range(97, 97 + sum(ok_lens)))
+    n = len(ok_lens)
+    cases = [
+        ("dlba_ok", _page_chunk(_dlba(ok_lens, chars), n, DLBA), 0),
+        # a negative length: make([]byte, size) panics in the reference -> BYTE_ARRAY
+        ("dlba_negative", _page_chunk(_dlba([3, -2, 5, 2, 7, 1, 4, 4, 2], chars), n, DLBA),
+         abi.STATUS_CODES["BYTE_ARRAY"]),
+        # lengths past the page: io.ReadFull short -> EOF
+        ("dlba_short", _page_chunk(_dlba(ok_lens, chars[:-3]), n, DLBA), abi.STATUS_CODES["EOF"]),
+        # fewer lengths than values: next() at position >= len(lens) -> EOF
+        ("dlba_few_lens", _page_chunk(_dlba(ok_lens[:5], chars[:sum(ok_lens[:5])]), n, DLBA),
+         abi.STATUS_CODES["EOF"]),
+        # Q3: one length, no miniblock header -> init fails (EOF)
+        ("dlba_one_value", _page_chunk(_dlba([3], b"abc"), 1, DLBA), abi.STATUS_CODES["EOF"]),
+        # more lengths than the page's values: refused
+        ("dlba_count_guard", _page_chunk(_dlba(ok_lens, chars), 4, DLBA), abi.STATUS_CODES["DELTA"]),
+        ("dba_ok", _page_chunk(_dba([0, 2, 2, 0, 1, 1, 0, 2, 2], ok_lens, chars), n, DBA), 0),
+        # prefix longer than the previous value -> "invalid prefix len in the stream"
+        ("dba_prefix_too_long", _page_chunk(_dba([0, 2, 2, 0, 9, 1, 0, 2, 2], ok_lens, chars), n, DBA),
+         abi.STATUS_CODES["BYTE_ARRAY"]),
+        # different numbers of prefixes and suffixes
+        ("dba_count_mismatch", _page_chunk(_dba([0, 2, 2, 0, 1, 1, 0, 2], ok_lens, chars), n, DBA),
+         abi.STATUS_CODES["DELTA"]),
+        # negative prefix + suffix capacity: panics in the reference -> BYTE_ARRAY
+        ("dba_negative_capacity", _page_chunk(_dba([0, -9, 2, 0, 1, 1, 0, 2, 2], ok_lens, chars), n, DBA),
+         abi.STATUS_CODES["BYTE_ARRAY"]),
+        # a negative prefix with a long enough suffix is a plain suffix (no check fails)
+        ("dba_negative_prefix", _page_chunk(_dba([0, 2, -1, 0, 1, 1, 0, 2, 2], ok_lens, chars), n, DBA), 0),
+    ]
+    return cases
+
+
+@pytest.mark.parametrize("case", hand_cases(), ids=lambda c: c[0])
+def test_oracle_hand_pages(case):
+    name, chunk, want = case
+    job, _ = U.chunk_job(chunk, ptype=abi.BYTE_ARRAY)
+    r = O.decode_chunk(job)
+    assert r.status == want, "%s: %s" % (name, abi.status_name(r.status))
+    if name == "dlba_ok":
+        assert b"".join(_strings(r)) == bytes(range(97, 97 + 28))
+    if name == "dba_ok":
+        got = _strings(r)
+        assert len(got) == 9 and got[1][:2] == got[0][:2]
+
+
+def test_flba_delta_byte_array_unsupported():
+    """DELTA_BYTE_ARRAY on FIXED_LEN_BYTE_ARRAY (chunk_reader.go:90-91) is not
+    built: both paths report UNSUPPORTED."""
+    chunk = _page_chunk(_dba([0, 1, 1, 0, 1, 1, 0, 2, 2], [4] * 9, bytes(36)), 9, DBA)
+    job, _ = U.chunk_job(chunk, ptype=abi.FIXED_LEN_BYTE_ARRAY, type_length=4)
+    assert O.decode_chunk(job).status == abi.STATUS_CODES["UNSUPPORTED"]
+
+
+# ---------------------------------------------------------------- GPU vs oracle
+@pytest.fixture(scope="module")
+def dec():
+    import pqgpu
+    d = pqgpu.GpuDecoder(0)
+    yield d
+    d.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", CASES, ids=lambda k: "e%d_v%d_c%d_n%d_s%d" % (
+    k["encoding"], k["page_version"], k["codec"], int(k["null_frac"] * 100), k["sorted_values"]))
+def test_gpu_generated_files(dec, kw):
+    import pqgpu
+    data, _ = W.config_delta_strings(rows=30000, rows_per_page=7000, **kw)
+    pf = pqgpu.ParquetFile(data)
+    dev = dec.upload(pf.data)
+    try:
+        r = dec.decode_jobs([pqgpu.device_job(pf, 0, 0, dev)])[0]
+        P.compare_chunk(P.oracle_chunk(pf, 0, 0), dec.download(r, 0), "delta strings")
+    finally:
+        dec.free(dev)
+
+
+@pytest.mark.gpu
+def test_gpu_long_values_and_shared_prefixes(dec):
+    """DELTA_BYTE_ARRAY values longer than the LDS buffers of k_str_dba (16 KiB
+    previous value, 8 KiB suffix stage) and long shared prefixes."""
+    rng = np.random.default_rng(12)
+    base = bytes(rng.integers(97, 123, 40000, dtype=np.uint8))
+    vals = sorted(base[:int(rng.integers(1, 40000))] + bytes([int(x)]) for x in rng.integers(97, 123, 300))
+    vals += [b"z" * 20000, b"z" * 20001 + b"a", b"y"]
+    offs = np.zeros(len(vals) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(v) for v in vals])
+    chars = np.frombuffer(b"".join(vals), dtype=np.uint8).copy()
+    for enc in (DBA, DLBA):
+        col = W.Column("s", abi.BYTE_ARRAY, chars, offsets=offs, encoding=enc, rows_per_page=120)
+        data = W.write_file([col], len(vals))
+        import pqgpu
+        pf = pqgpu.ParquetFile(data)
+        exp = P.oracle_chunk(pf, 0, 0)
+        assert exp.status == 0 and _strings(exp) == vals
+        dev = dec.upload(pf.data)
+        try:
+            r = dec.decode_jobs([pqgpu.device_job(pf, 0, 0, dev)])[0]
+            P.compare_chunk(exp, dec.download(r, 0), "long values enc %d" % enc)
+        finally:
+            dec.free(dev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", hand_cases(), ids=lambda c: c[0])
+def test_gpu_hand_pages(dec, case):
+    P.compare_chunk_bytes(case[1], dec, ptype=abi.BYTE_ARRAY)
+
+
+@pytest.mark.gpu
+def test_gpu_mutations(dec):
+    """Random byte flips in DLBA / DBA pages: the same status, error page and bytes as the oracle."""
+    rng = np.random.default_rng(13)
+    for enc in (DLBA, DBA):
+        data, _ = W.config_delta_strings(rows=3000, rows_per_page=700, encoding=enc, codec=W.UNCOMPRESSED,
+                                         null_frac=0.1)
+        import pqgpu
+        pf = pqgpu.ParquetFile(data)
+        m = pf.chunk_meta(0, 0)
+        chunk = bytes(pf.data[m.start:m.start + m.total_compressed_size])
+        d = pf.columns[0].desc
+        for _ in range(40):
+            b = bytearray(chunk)
+            for _ in range(int(rng.integers(1, 4))):
+                b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+            P.compare_chunk_bytes(bytes(b), dec, ptype=abi.BYTE_ARRAY, max_def=d.max_def)
