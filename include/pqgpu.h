@@ -394,6 +394,21 @@ int pqg_file_column(const pqg_file* f, int col, pqg_column_info* out);
 int pqg_file_chunk(const pqg_file* f, int row_group, int col, pqg_chunk_meta* out);
 int64_t pqg_file_row_group_rows(const pqg_file* f, int row_group);
 
+/* The schema tree below the root, depth first (makeSchema / readGroupSchema
+ * schema.go:789-894, 996-1025): what NextRow's row assembly walks
+ * (Column.getData schema.go:171-264).  Replaces the Column tree the reference
+ * builds for FileReader. */
+typedef struct pqg_schema_node {
+  char name[128];
+  int32_t repetition;    /* 0 REQUIRED, 1 OPTIONAL, 2 REPEATED */
+  int32_t num_children;  /* 0 for a leaf */
+  int32_t leaf;          /* column index of a leaf (pqg_file_column), -1 for a group */
+  int32_t max_def, max_rep;
+  int32_t reserved;
+} pqg_schema_node;
+int pqg_file_num_schema_nodes(const pqg_file* f);
+int pqg_file_schema_node(const pqg_file* f, int i, pqg_schema_node* out);
+
 /* ======================= oracle (TEST INFRASTRUCTURE) ===================== */
 /* Implemented only by oracle/liboracle.so.  Host pointers everywhere. */
 int pqo_decode_chunk(const pqg_chunk_job* job, pqg_chunk_result* res,

@@ -7,6 +7,7 @@
 // (+1 per REPEATED element).  Row group r's chunk for leaf i is
 // RowGroup.columns[i] (readRowGroup chunk_reader.go:404-431).
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -168,8 +169,14 @@ struct Parser {
 
 }  // namespace
 
+struct SNode {
+  std::string name;
+  int32_t rep, num_children, leaf, max_def, max_rep;
+};
+
 struct pqg_file {
   std::vector<Leaf> leaves;
+  std::vector<SNode> nodes;  // schema tree below the root, depth first
   std::vector<std::vector<ChunkM>> rgs;
   std::vector<int64_t> rg_rows;
   int64_t num_rows = 0;
@@ -179,7 +186,7 @@ namespace {
 
 // schema.go:789-894 (readColumnSchema / readGroupSchema), depth-first.
 bool read_schema(const std::vector<Elem>& s, size_t& idx, const std::string& name, int d, int r,
-                 std::vector<Leaf>& out, int depth) {
+                 std::vector<Leaf>& out, int depth, std::vector<SNode>& nodes) {
   if (depth > 256 || idx >= s.size()) return false;
   const Elem& e = s[idx];
   if (!e.has_type) {  // group
@@ -188,9 +195,10 @@ bool read_schema(const std::vector<Elem>& s, size_t& idx, const std::string& nam
     if (e.has_rep && e.rep != 0) d++;
     if (e.has_rep && e.rep == 2) r++;
     std::string nm = name.empty() ? e.name : name + "." + e.name;
+    nodes.push_back(SNode{e.name, e.has_rep ? e.rep : 0, e.num_children, -1, d, r});
     idx++;
     for (int i = 0; i < e.num_children; i++)
-      if (!read_schema(s, idx, nm, d, r, out, depth + 1)) return false;
+      if (!read_schema(s, idx, nm, d, r, out, depth + 1, nodes)) return false;
     return true;
   }
   if (e.name.empty() || !e.has_rep) return false;
@@ -210,6 +218,7 @@ bool read_schema(const std::vector<Elem>& s, size_t& idx, const std::string& nam
     uns = true;
   l.desc.flags = uns ? 1 : 0;
   l.path = name.empty() ? e.name : name + "." + e.name;
+  nodes.push_back(SNode{e.name, e.rep, 0, (int32_t)out.size(), d, r});
   out.push_back(l);
   idx++;
   return true;
@@ -296,7 +305,7 @@ static int open_footer(const uint8_t* footer, int32_t fl, pqg_file** out) {
   pqg_file* f = new pqg_file();
   size_t idx = 1;  // makeSchema: readSchema(meta.Schema[1:])
   while (idx < schema.size()) {
-    if (!read_schema(schema, idx, "", 0, 0, f->leaves, 0)) {
+    if (!read_schema(schema, idx, "", 0, 0, f->leaves, 0, f->nodes)) {
       delete f;
       return PQG_ERR_METADATA;
     }
@@ -315,6 +324,21 @@ int64_t pqg_file_num_rows(const pqg_file* f) { return f ? f->num_rows : 0; }
 int64_t pqg_file_row_group_rows(const pqg_file* f, int rg) {
   if (!f || rg < 0 || rg >= (int)f->rgs.size()) return -1;
   return f->rg_rows[(size_t)rg];
+}
+
+int pqg_file_num_schema_nodes(const pqg_file* f) { return f ? (int)f->nodes.size() : PQG_ERR_INVALID_ARG; }
+
+int pqg_file_schema_node(const pqg_file* f, int i, pqg_schema_node* out) {
+  if (!f || !out || i < 0 || i >= (int)f->nodes.size()) return PQG_ERR_INVALID_ARG;
+  memset(out, 0, sizeof(*out));
+  const SNode& n = f->nodes[(size_t)i];
+  snprintf(out->name, sizeof(out->name), "%s", n.name.c_str());
+  out->repetition = n.rep;
+  out->num_children = n.num_children;
+  out->leaf = n.leaf;
+  out->max_def = n.max_def;
+  out->max_rep = n.max_rep;
+  return PQG_OK;
 }
 
 int pqg_file_column(const pqg_file* f, int col, pqg_column_info* out) {

@@ -52,6 +52,8 @@ def lib():
         "pqg_file_row_group_rows": ([P, I], I64),
         "pqg_file_column": ([P, I, C.POINTER(abi.ColumnInfo)], I),
         "pqg_file_chunk": ([P, I, I, C.POINTER(abi.ChunkMeta)], I),
+        "pqg_file_num_schema_nodes": ([P], I),
+        "pqg_file_schema_node": ([P, I, C.POINTER(abi.SchemaNode)], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -68,5 +70,5 @@ EXPORTED = [
     "pqg_assemble_list", "pqg_decode_page", "pqg_block_decompress", "pqg_pack_levels", "pqg_file_open", "pqg_file_open_tail",
     "pqg_file_close",
     "pqg_file_num_columns", "pqg_file_num_row_groups", "pqg_file_num_rows", "pqg_file_row_group_rows",
-    "pqg_file_column", "pqg_file_chunk",
+    "pqg_file_column", "pqg_file_chunk", "pqg_file_num_schema_nodes", "pqg_file_schema_node",
 ]

@@ -122,6 +122,11 @@ class ColumnInfo(C.Structure):
     _fields_ = [("desc", ColumnDesc), ("path", C.c_char * 256)]
 
 
+class SchemaNode(C.Structure):
+    _fields_ = [("name", C.c_char * 128), ("repetition", C.c_int32), ("num_children", C.c_int32),
+                ("leaf", C.c_int32), ("max_def", C.c_int32), ("max_rep", C.c_int32), ("reserved", C.c_int32)]
+
+
 class ChunkMeta(C.Structure):
     _fields_ = [
         ("start", C.c_int64),

@@ -68,6 +68,11 @@ class ParquetFile:
             ci = abi.ColumnInfo()
             _check(L.pqg_file_column(h, i, C.byref(ci)), "pqg_file_column")
             self.columns.append(ci)
+        self.schema_nodes = []  # depth first, below the root (pqg_file_schema_node)
+        for i in range(L.pqg_file_num_schema_nodes(h)):
+            sn = abi.SchemaNode()
+            _check(L.pqg_file_schema_node(h, i, C.byref(sn)), "pqg_file_schema_node")
+            self.schema_nodes.append(sn)
 
     @classmethod
     def open(cls, path):
@@ -359,6 +364,7 @@ class FileReader:
         self.selected = self._select(columns)
         self.row_group_position = 0
         self.uploaded_bytes = 0   # H2D bytes so far (projection pushdown check)
+        self._rows = None         # NextRow state (pqgpu.rows.RowReader)
 
     def _select(self, columns):
         if not columns:
@@ -402,6 +408,27 @@ class FileReader:
             res = self.dec.decode_jobs(jobs)
             return {self.file.columns[c].path.decode(): self.dec.download(r, i)
                     for i, ((_, c), r) in enumerate(zip(specs, res))}
+        finally:
+            self.dec.free(dev)
+
+    def next_row(self):
+        """NextRow (file_reader.go:101-108): the next row of the selected
+        columns as a dict (pqgpu.rows), decoding the next row group on the GPU
+        when the current one is used up; EOFError after the last row."""
+        if self._rows is None:
+            from .rows import RowReader
+            self._rows = RowReader(self.file, self.selected, self._decode_for_rows)
+        return self._rows.next_row()
+
+    def _decode_for_rows(self, rg):
+        specs = [(rg, c) for c in self.selected]
+        if not specs:
+            return {}
+        jobs, dev, nbytes = span_jobs(self.file, specs, self.dec)
+        self.uploaded_bytes += nbytes
+        try:
+            res = self.dec.decode_jobs(jobs)
+            return {c: self.dec.download(r, i) for i, ((_, c), r) in enumerate(zip(specs, res))}
         finally:
             self.dec.free(dev)
 
