@@ -43,15 +43,22 @@ namespace pqg {
 constexpr int kDWaves = PQG_DICT_WAVES; // waves per workgroup = pages per queue item
 constexpr int kDictLdsEntries = 4096;   // dictionaries gathered from LDS (16 KiB)
 constexpr int kPBlocks = 63;            // blocks per piece (lane 63's descriptor bounds the last one)
-constexpr int kPRuns = 256;             // run entries per piece
+#ifndef PQG_DICT_PRUNS
+#define PQG_DICT_PRUNS 256
+#endif
+constexpr int kPRuns = PQG_DICT_PRUNS;   // run entries per piece (a multiple of 128)
 constexpr int kPPay = PQG_DICT_PPAY;    // payload bytes per piece
+#ifndef PQG_DICT_FLUSH
+#define PQG_DICT_FLUSH 2
+#endif
+constexpr int kFlushBlocks = PQG_DICT_FLUSH;  // blocks decoded into obuf per flush
 constexpr int kPG = kPPay / 1024;       // payload granules per lane
 constexpr int kPRunGr = kPRuns / 128;   // run-table granules per lane
 
 struct PieceShared {
   RunEnt runs[kPRunGr * 128];       // from the 16-byte granule holding the piece's first run
   uint32_t stage[kPG * 256 + 4];    // payload window from a 16-byte aligned address (+ a dword past it)
-  uint32_t obuf[2 * kHBlock + 8];   // values of a block pair (+ <= 3 dwords carried), see OutState
+  uint32_t obuf[kFlushBlocks * kHBlock + 8];  // values of the blocks of a flush (+ <= 3 dwords carried), see OutState
   uint8_t rmap[kHBlock];            // run starting at each value of a multi-run block
   uint8_t ridx[kHBlock];            // run of each value of a multi-run block
 };
@@ -228,7 +235,7 @@ __device__ __forceinline__ void flush_obuf(PieceShared& ps, OutState& os, uint32
   const uint32_t full = total >> 2;
   const PQG_L u32x4_t* ob4 = (const PQG_L u32x4_t*)lds_ptr(ps.obuf);
 #pragma unroll
-  for (int k = 0; k < (2 * kHBlock + 4) / 256 + 1; k++) {
+  for (int k = 0; k < (kFlushBlocks * kHBlock + 4) / 256 + 1; k++) {
     const uint32_t g = (uint32_t)(lane + 64 * k);
     if (g < full) {
       const u32x4_t x = ob4[g];
@@ -332,25 +339,26 @@ __device__ __forceinline__ int64_t dict_page(PieceShared& ps, const gcu8 sp, con
       continue;
     }
     const int64_t plo8 = plo * 8;
-    // ---- blocks of the piece, two per flush
-    for (int k0 = 0; k0 < m; k0 += 2) {
+    // ---- blocks of the piece, kFlushBlocks per flush
+    for (int k0 = 0; k0 < m; k0 += kFlushBlocks) {
       PQG_DT(tp0);
-      PBlock B[2];
+      uint32_t tot = os.carry;
 #pragma unroll
-      for (int b = 0; b < 2; b++) {
-        const int k = k0 + b < m ? k0 + b : m - 1;
-        B[b].on = k0 + b < m;
-        B[b].v0 = (uint32_t)__builtin_amdgcn_readlane((int)v0, k);
+      for (int b = 0; b < kFlushBlocks; b++) {
+        if (k0 + b >= m) break;
+        const int k = k0 + b;
+        PBlock B;
+        B.on = true;
+        B.v0 = (uint32_t)__builtin_amdgcn_readlane((int)v0, k);
         const uint32_t nx = (uint32_t)__builtin_amdgcn_readlane((int)v0, k + 1);
-        B[b].v1 = nx < end_all ? nx : end_all;
-        B[b].rl = (uint32_t)__builtin_amdgcn_readlane((int)r0, k) - rcur + (uint32_t)rskew;
-        B[b].nr = (uint32_t)__builtin_amdgcn_readlane((int)nr, k);
+        B.v1 = nx < end_all ? nx : end_all;
+        B.rl = (uint32_t)__builtin_amdgcn_readlane((int)r0, k) - rcur + (uint32_t)rskew;
+        B.nr = (uint32_t)__builtin_amdgcn_readlane((int)nr, k);
+        block_to_obuf(ps, B, mask, w, plo8, lane, tot, dcount, dict, bad);
+        tot += B.v1 - B.v0;
       }
-      const uint32_t n0 = B[0].v1 - B[0].v0, n1 = B[1].on ? B[1].v1 - B[1].v0 : 0u;
-      block_to_obuf(ps, B[0], mask, w, plo8, lane, os.carry, dcount, dict, bad);
-      if (B[1].on) block_to_obuf(ps, B[1], mask, w, plo8, lane, os.carry + n0, dcount, dict, bad);
       PQG_DT(tp2);
-      flush_obuf(ps, os, os.carry + n0 + n1, lane);
+      flush_obuf(ps, os, tot, lane);
       PQG_DT(tp3);
       pf.add(11, tp2 - tp0);
       pf.add(12, tp3 - tp2);

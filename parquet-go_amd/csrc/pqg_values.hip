@@ -174,7 +174,12 @@ struct BoolSink {
 constexpr int kBlocks = 64;
 constexpr int kMaxMb = 8;
 
+#ifndef PQG_DBP_STAGE
+#define PQG_DBP_STAGE 4096
+#endif
+constexpr int kDStage = PQG_DBP_STAGE;  // staged bytes of the regular path (a multiple of 1024)
 struct DbpShared {
+  uint8_t stage[kDStage + 16];          // regular path: block headers and bodies
   uint8_t win[kWin];
   int64_t body[kBlocks];                // stream offset of the block's first miniblock
   uint64_t mind[kBlocks];               // min delta (as unsigned for wrapping adds)
@@ -184,101 +189,55 @@ struct DbpShared {
   uint64_t gvals[8];                    // generic path: current 8-group
 };
 
-// Values of a DBP page: emulates deltaBitPackDecoder{32,64}.next for positions
-// [0, nn).  Regular layout (miniblock value count a multiple of 8, <= kMaxMb
-// miniblocks): wave-parallel unpack + wrapping scan; otherwise one lane.
-__device__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_t nn, gu8 out,
-                          DbpShared& sh, int stage /*0 = header only (read phase), 1 = decode*/) {
+// Stage [at, at + kDStage) of a DBP stream (from a 16-byte aligned address;
+// bytes at or past n read as zero) into LDS with one round of loads.
+__device__ __forceinline__ void dbp_restage(gcu8 s, int64_t n, PQG_L uint8_t* stb, int64_t at, int64_t& st_lo,
+                                            int64_t& st_hi) {
   const int lane = lane_id();
-  Window win{s, n, kFarAway, lds_ptr(sh.win)};
-  int64_t pos = 0;
-  int32_t bs, mbc, total;
-  uint64_t first;
-  int e;
-  // readBlockHeader
-  if ((e = read_u32var_delta(win, pos, &bs))) return e;
-  if (bs <= 0 && bs % 128 != 0) return kDELTA;
-  if ((e = read_u32var_delta(win, pos, &mbc))) return e;
-  if (mbc <= 0 || bs % mbc != 0) return kDELTA;
-  int32_t mbvc = bs / mbc;
-  if (mbvc == 0) return kDELTA;
-  if ((e = read_u32var_delta(win, pos, &total))) return e;
-  if ((e = read_signed(win, pos, is64, &first))) return e;
+  st_lo = at - (int64_t)(((uintptr_t)(s + at)) & 15);
+  uint4 g[kDStage / 1024];
+#pragma unroll
+  for (int k = 0; k < kDStage / 1024; k++) {
+    const int64_t o = st_lo + 16 * (int64_t)(lane + 64 * k);
+    g[k] = (o < n && o + 16 > 0) ? ldg16((uintptr_t)(s + o)) : make_uint4(0u, 0u, 0u, 0u);
+  }
+#pragma unroll
+  for (int k = 0; k < kDStage / 1024; k++) {
+    const int64_t o = st_lo + 16 * (int64_t)(lane + 64 * k);
+    sts16(stb + 16 * (lane + 64 * k), mask_tail(g[k], o, n));
+  }
+  st_hi = st_lo + kDStage;
+  __builtin_amdgcn_wave_barrier();
+}
+// binary.ReadUvarint over the stage (bytes at or past n: EOF)
+__device__ __forceinline__ int dbp_st_uvarint(const PQG_L uint8_t* stb, int64_t st_lo, int64_t n, int64_t& q,
+                                              uint64_t* out) {
+  uint64_t x = 0;
+  unsigned sft = 0;
+  for (int i = 0;; i++) {
+    if (q >= n) return kEOF;
+    const uint32_t bt = stb[q - st_lo];
+    q++;
+    if (bt < 0x80) {
+      if (i > 9 || (i == 9 && bt > 1)) return kRLE;
+      *out = x | (sft < 64 ? (uint64_t)bt << sft : 0);
+      return kOK;
+    }
+    if (sft < 64) x |= (uint64_t)(bt & 0x7f) << sft;
+    sft += 7;
+  }
+}
+
+// The regular-layout block walk through a Window, resuming at position p0 /
+// block header blk_pos / value carry: for blocks too large for dbp_decode's
+// stage (the fast path's fallback; the same semantics).
+__device__ __forceinline__ int dbp_decode_rest(gcu8 s, int64_t n, int64_t readable, bool is64, int64_t nn, gu8 out, DbpShared& sh,
+                               int64_t P, int64_t p0, int64_t blk_pos, uint64_t carry, int32_t bs, int32_t mbc,
+                               int32_t mbvc, int32_t total, bool pow2, int bs_sh, int mb_sh) {
+  const int lane = lane_id();
   const int maxw = is64 ? 64 : 32;
-  // first readMiniBlockHeader (part of init)
-  {
-    int64_t p = pos;
-    uint64_t md;
-    if ((e = read_signed(win, p, is64, &md))) return e;
-    if (n - p < mbc) return kEOF;
-    for (int m = 0; m < mbc; m++)
-      if (win.get(p + m) > maxw) return kBIT_WIDTH;
-  }
-  if (stage == 0) return kOK;
-  const int64_t P = nn < total ? nn : total;  // positions actually produced before EOF
-  const bool regular = (mbvc % 8 == 0) && mbc <= kMaxMb && bs <= (1 << 24);
-  const bool pow2 = (bs & (bs - 1)) == 0 && (mbvc & (mbvc - 1)) == 0;
-  const int bs_sh = __builtin_ctz((uint32_t)bs), mb_sh = __builtin_ctz((uint32_t)mbvc);
-  if (!regular) {
-    // ---- generic single-lane emulation of next() (rare layouts)
-    int64_t rp = pos;
-    int32_t cur_mb = mbc;  // force header read at position 0 semantics below
-    uint64_t mind = 0, prev = first;
-    uint8_t* widths = sh.gwidths;  // LDS: wave-uniform values (no scratch)
-    uint64_t* vals = sh.gvals;
-    int32_t cw = 0, mbpos = 0;
-    for (int k = 0; k < 8; k++) vals[k] = 0;
-    // init already read the first miniblock header: emulate it
-    {
-      if ((e = read_signed(win, rp, is64, &mind))) return e;
-      for (int m = 0; m < mbc && m < 256; m++) widths[m] = (uint8_t)win.get(rp + m);
-      if (mbc > 256) return kUNSUPPORTED;
-      rp += mbc;
-      cur_mb = 0;
-    }
-    for (int64_t p = 0; p < nn; p++) {
-      if (p >= total) return kEOF;
-      if (p % 8 == 0) {
-        if (p % mbvc == 0) {
-          if (cur_mb >= mbc) {
-            if ((e = read_signed(win, rp, is64, &mind))) return e;
-            if (n - rp < mbc) return kEOF;
-            for (int m = 0; m < mbc; m++) {
-              int wv = win.get(rp + m);
-              if (wv > maxw) return kBIT_WIDTH;
-              widths[m] = (uint8_t)wv;
-            }
-            rp += mbc;
-            cur_mb = 0;
-          }
-          cw = widths[cur_mb];
-          mbpos = 0;
-          cur_mb++;
-        }
-        if (n - rp < cw) return kEOF;
-        for (int k = 0; k < 8; k++) vals[k] = extract_bits64(s, readable, n, rp * 8 + (int64_t)k * cw, cw);
-        rp += cw;
-        mbpos += cw;
-        if (p + 8 >= total) {
-          int64_t l = (int64_t)(mbvc / 8) * cw - mbpos;
-          if (l < 0) return kDELTA;
-          rp += l;  // padding skip, errors ignored
-          if (rp > n) rp = n;
-        }
-      }
-      if (lane == 0) {
-        if (is64) stg8((uintptr_t)(out + p * 8), (uint32_t)prev, (uint32_t)(prev >> 32));
-        else *(PQG_G uint32_t*)(out + p * 4) = (uint32_t)prev;
-      }
-      prev = prev + vals[p % 8] + mind;
-      if (!is64) prev = (uint32_t)prev;
-    }
-    return kOK;
-  }
-  // ---- regular layout: walk blocks in batches, then unpack + scan
-  uint64_t carry = first;  // value at the first position of the next tile
-  int64_t blk_pos = pos;   // stream offset of the next block header
-  int64_t p0 = 0;          // first position of the current batch
+  Window win{s, n, kFarAway, lds_ptr(sh.win)};
+  int e;
   bool first_block = true;
   while (p0 < P) {
     int nb = 0;
@@ -377,6 +336,234 @@ __device__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_
           run += d[k];
         }
         store_run_aligned<4>((uintptr_t)(out + t0 * 4), dw, nvp);
+      }
+      carry += __shfl(incl, 63, 64);
+    }
+    __builtin_amdgcn_wave_barrier();
+    p0 = p_end;
+  }
+  if (nn > total) return kEOF;
+  return kOK;
+}
+
+// Values of a DBP page: emulates deltaBitPackDecoder{32,64}.next for positions
+// [0, nn).  Regular layout (miniblock value count a multiple of 8, <= kMaxMb
+// miniblocks): wave-parallel unpack + wrapping scan; otherwise one lane.
+__device__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_t nn, gu8 out,
+                          DbpShared& sh, int stage /*0 = header only (read phase), 1 = decode*/) {
+  const int lane = lane_id();
+  Window win{s, n, kFarAway, lds_ptr(sh.win)};
+  int64_t pos = 0;
+  int32_t bs, mbc, total;
+  uint64_t first;
+  int e;
+  // readBlockHeader
+  if ((e = read_u32var_delta(win, pos, &bs))) return e;
+  if (bs <= 0 && bs % 128 != 0) return kDELTA;
+  if ((e = read_u32var_delta(win, pos, &mbc))) return e;
+  if (mbc <= 0 || bs % mbc != 0) return kDELTA;
+  int32_t mbvc = bs / mbc;
+  if (mbvc == 0) return kDELTA;
+  if ((e = read_u32var_delta(win, pos, &total))) return e;
+  if ((e = read_signed(win, pos, is64, &first))) return e;
+  const int maxw = is64 ? 64 : 32;
+  // first readMiniBlockHeader (part of init)
+  {
+    int64_t p = pos;
+    uint64_t md;
+    if ((e = read_signed(win, p, is64, &md))) return e;
+    if (n - p < mbc) return kEOF;
+    for (int m = 0; m < mbc; m++)
+      if (win.get(p + m) > maxw) return kBIT_WIDTH;
+  }
+  if (stage == 0) return kOK;
+  const int64_t P = nn < total ? nn : total;  // positions actually produced before EOF
+  const bool regular = (mbvc % 8 == 0) && mbc <= kMaxMb && bs <= (1 << 24);
+  const bool pow2 = (bs & (bs - 1)) == 0 && (mbvc & (mbvc - 1)) == 0;
+  const int bs_sh = __builtin_ctz((uint32_t)bs), mb_sh = __builtin_ctz((uint32_t)mbvc);
+  if (!regular) {
+    // ---- generic single-lane emulation of next() (rare layouts)
+    int64_t rp = pos;
+    int32_t cur_mb = mbc;  // force header read at position 0 semantics below
+    uint64_t mind = 0, prev = first;
+    uint8_t* widths = sh.gwidths;  // LDS: wave-uniform values (no scratch)
+    uint64_t* vals = sh.gvals;
+    int32_t cw = 0, mbpos = 0;
+    for (int k = 0; k < 8; k++) vals[k] = 0;
+    // init already read the first miniblock header: emulate it
+    {
+      if ((e = read_signed(win, rp, is64, &mind))) return e;
+      for (int m = 0; m < mbc && m < 256; m++) widths[m] = (uint8_t)win.get(rp + m);
+      if (mbc > 256) return kUNSUPPORTED;
+      rp += mbc;
+      cur_mb = 0;
+    }
+    for (int64_t p = 0; p < nn; p++) {
+      if (p >= total) return kEOF;
+      if (p % 8 == 0) {
+        if (p % mbvc == 0) {
+          if (cur_mb >= mbc) {
+            if ((e = read_signed(win, rp, is64, &mind))) return e;
+            if (n - rp < mbc) return kEOF;
+            for (int m = 0; m < mbc; m++) {
+              int wv = win.get(rp + m);
+              if (wv > maxw) return kBIT_WIDTH;
+              widths[m] = (uint8_t)wv;
+            }
+            rp += mbc;
+            cur_mb = 0;
+          }
+          cw = widths[cur_mb];
+          mbpos = 0;
+          cur_mb++;
+        }
+        if (n - rp < cw) return kEOF;
+        for (int k = 0; k < 8; k++) vals[k] = extract_bits64(s, readable, n, rp * 8 + (int64_t)k * cw, cw);
+        rp += cw;
+        mbpos += cw;
+        if (p + 8 >= total) {
+          int64_t l = (int64_t)(mbvc / 8) * cw - mbpos;
+          if (l < 0) return kDELTA;
+          rp += l;  // padding skip, errors ignored
+          if (rp > n) rp = n;
+        }
+      }
+      if (lane == 0) {
+        if (is64) stg8((uintptr_t)(out + p * 8), (uint32_t)prev, (uint32_t)(prev >> 32));
+        else *(PQG_G uint32_t*)(out + p * 4) = (uint32_t)prev;
+      }
+      prev = prev + vals[p % 8] + mind;
+      if (!is64) prev = (uint32_t)prev;
+    }
+    return kOK;
+  }
+  // ---- regular layout: block headers and bodies read from an LDS stage of
+  // kDStage bytes, refilled with one round of loads whenever the next block is
+  // not inside it; blocks walked in batches of <= kBlocks, then every position
+  // of the batch unpacked from the stage and scanned.
+  uint64_t carry = first;  // value at the first position of the next tile
+  int64_t blk_pos = pos;   // stream offset of the next block header
+  int64_t p0 = 0;          // first position of the current batch
+  int64_t st_lo = kFarAway, st_hi = kFarAway;  // staged stream range (st_lo: a 16-byte aligned address)
+  PQG_L uint8_t* const stb = lds_ptr(sh.stage);
+  while (p0 < P) {
+    int nb = 0;
+    int64_t p_end = p0;
+    bool fresh = false;  // the stage was just filled at blk_pos
+    while (nb < kBlocks && p_end < P) {
+      // the header (<= 10 varint bytes + mbc widths) must be staged
+      if (!(blk_pos >= st_lo && blk_pos + 10 + mbc <= st_hi)) {
+        if (nb > 0) break;  // decode the batch so far, then restage here
+        dbp_restage(s, n, stb, blk_pos, st_lo, st_hi);
+        fresh = true;
+      }
+      // block header: min delta + widths (readMiniBlockHeader)
+      int64_t hp = blk_pos;
+      uint64_t ux;
+      int ev = dbp_st_uvarint(stb, st_lo, n, hp, &ux);
+      if (ev) return ev == kEOF ? kEOF : kDELTA;
+      int64_t mdv = (int64_t)(ux >> 1);
+      if (ux & 1) mdv = ~mdv;
+      if (!is64 && (mdv > 2147483647LL || mdv < -2147483648LL)) return kDELTA;
+      const uint64_t md = (uint64_t)mdv;
+      if (n - hp < mbc) return kEOF;
+      // groups of this block that positions < P read: each must be whole
+      const int64_t bp0 = p_end;
+      const int64_t bp1 = bp0 + bs < P ? bp0 + bs : P;
+      const int64_t rel = ((bp1 - 1) / 8) * 8 - bp0;  // the last group read
+      const int m_last = (int)(rel / mbvc);
+      const int64_t g_in_mb = (rel % mbvc) / 8;
+      int64_t off = hp + mbc, mo_last = 0;
+      int w_last = 0;
+      for (int m = 0; m < mbc; m++) {
+        const int wv = stb[hp + m - st_lo];
+        if (wv > maxw) return kBIT_WIDTH;
+        if (m == m_last) {
+          w_last = wv;
+          mo_last = off;
+        }
+        if (lane == 0) {
+          sh.widths[nb][m] = (uint8_t)wv;
+          sh.mb_off[nb][m] = off - st_lo;  // stage byte of the miniblock
+        }
+        off += (int64_t)(mbvc / 8) * wv;
+      }
+      const int64_t g_end = mo_last + (g_in_mb + 1) * w_last;
+      if (g_end > n) return kEOF;
+      if (g_end > st_hi) {  // the block's body is not staged
+        if (nb > 0) break;
+        if (fresh) return dbp_decode_rest(s, n, readable, is64, nn, out, sh, P, p0, blk_pos, carry, bs, mbc, mbvc,
+                                          total, pow2, bs_sh, mb_sh);
+        dbp_restage(s, n, stb, blk_pos, st_lo, st_hi);
+        fresh = true;
+        continue;
+      }
+      if (lane == 0) sh.mind[nb] = md;
+      nb++;
+      p_end = bp1;
+      blk_pos = off;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // unpack + wrapping prefix over positions [p0, p_end): value(p) = carry + sum of deltas.
+    // A lane's 4 positions share one miniblock (mbvc % 8 == 0): the block /
+    // miniblock split once per lane, by shifts for power-of-two sizes.
+    const PQG_L uint32_t* stw = (const PQG_L uint32_t*)stb;
+    for (int64_t t0 = p0; t0 < p_end; t0 += 256) {
+      uint64_t d[4];
+      uint64_t local = 0;
+      const int64_t pb = t0 + lane * 4;
+      const uint32_t rl = (uint32_t)(pb - p0);  // < kBlocks * bs <= 2^31 (regular)
+      uint32_t b, r2, m, j;
+      if (pow2) {
+        b = rl >> bs_sh;
+        r2 = rl & (uint32_t)(bs - 1);
+        m = r2 >> mb_sh;
+        j = r2 & (uint32_t)(mbvc - 1);
+      } else {
+        b = rl / (uint32_t)bs;
+        r2 = rl - b * (uint32_t)bs;
+        m = r2 / (uint32_t)mbvc;
+        j = r2 - m * (uint32_t)mbvc;
+      }
+      const bool any = pb < p_end;
+      const int wv = any ? sh.widths[b][m] : 0;
+      const uint32_t bit0 = any ? (uint32_t)sh.mb_off[b][m] * 8 + j * (uint32_t)wv : 0u;
+      const uint64_t mnd = any ? sh.mind[b] : 0;
+      const uint64_t wmask = wv == 64 ? ~0ull : ((1ull << wv) - 1);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint64_t dv = 0;
+        if (pb + k < p_end) {
+          const uint32_t bt = bit0 + (uint32_t)(k * wv);
+          const uint32_t dw = bt >> 5, sh5 = bt & 31;
+          const uint64_t lo = (uint64_t)stw[dw] | ((uint64_t)stw[dw + 1] << 32);
+          uint64_t x = lo >> sh5;
+          if (sh5 + wv > 64) x |= (uint64_t)stw[dw + 2] << (64 - sh5);
+          dv = (wv ? (x & wmask) : 0) + mnd;
+        }
+        d[k] = dv;
+        local += dv;
+      }
+      uint64_t incl = wave_incl_scan_u64(local);
+      uint64_t run = carry + (incl - local);
+      const int nvp = pb >= p_end ? 0 : (p_end - pb >= 4 ? 4 : (int)(p_end - pb));
+      if (is64) {
+        uint32_t dw8[8];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          dw8[2 * k] = (uint32_t)run;
+          dw8[2 * k + 1] = (uint32_t)(run >> 32);
+          run += d[k];
+        }
+        store_run_aligned<8>((uintptr_t)(out + t0 * 8), dw8, 2 * nvp);
+      } else {
+        uint32_t dw4[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          dw4[k] = (uint32_t)run;
+          run += d[k];
+        }
+        store_run_aligned<4>((uintptr_t)(out + t0 * 4), dw4, nvp);
       }
       carry += __shfl(incl, 63, 64);
     }
