@@ -308,13 +308,18 @@ __device__ __forceinline__ int64_t wave_min(int64_t v) {
   }
   return v;
 }
-// inclusive scan of uint64 (wrapping)
+// inclusive scan of uint64 (wrapping): DPP row_shr 1/2/4/8 then row_bcast
+// 15/31 on both halves, one 64-bit add per step (no LDS round trips)
 __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
-  int l = lane_id();
-  for (int o = 1; o < 64; o <<= 1) {
-    uint64_t t = __shfl_up(v, o, 64);
-    if (l >= o) v += t;
+#define PQG_SCAN64_STEP(ctrl, rm, bc)                                                             \
+  {                                                                                               \
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, ctrl, rm, 0xf, bc);  \
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), ctrl, rm, 0xf, bc); \
+    v += (uint64_t)hi << 32 | lo;                                                                 \
   }
+  PQG_SCAN64_STEP(0x111, 0xf, true) PQG_SCAN64_STEP(0x112, 0xf, true) PQG_SCAN64_STEP(0x114, 0xf, true)
+  PQG_SCAN64_STEP(0x118, 0xf, true) PQG_SCAN64_STEP(0x142, 0xa, false) PQG_SCAN64_STEP(0x143, 0xc, false)
+#undef PQG_SCAN64_STEP
   return v;
 }
 __device__ __forceinline__ int64_t wave_excl_scan_i64(int64_t v, int64_t* total) {

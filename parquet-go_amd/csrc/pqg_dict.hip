@@ -32,7 +32,7 @@
 namespace pqg {
 
 #ifndef PQG_DICT_PPAY
-#define PQG_DICT_PPAY 8192
+#define PQG_DICT_PPAY 4096
 #endif
 #ifndef PQG_DICT_WAVES
 #define PQG_DICT_WAVES 4
@@ -44,12 +44,12 @@ constexpr int kDWaves = PQG_DICT_WAVES; // waves per workgroup = pages per queue
 constexpr int kDictLdsEntries = 4096;   // dictionaries gathered from LDS (16 KiB)
 constexpr int kPBlocks = 63;            // blocks per piece (lane 63's descriptor bounds the last one)
 #ifndef PQG_DICT_PRUNS
-#define PQG_DICT_PRUNS 256
+#define PQG_DICT_PRUNS 128
 #endif
 constexpr int kPRuns = PQG_DICT_PRUNS;   // run entries per piece (a multiple of 128)
 constexpr int kPPay = PQG_DICT_PPAY;    // payload bytes per piece
 #ifndef PQG_DICT_FLUSH
-#define PQG_DICT_FLUSH 2
+#define PQG_DICT_FLUSH 1
 #endif
 constexpr int kFlushBlocks = PQG_DICT_FLUSH;  // blocks decoded into obuf per flush
 constexpr int kPG = kPPay / 1024;       // payload granules per lane

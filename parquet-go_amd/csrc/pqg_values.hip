@@ -179,10 +179,12 @@ constexpr int kMaxMb = 8;
 #endif
 constexpr int kDStage = PQG_DBP_STAGE;  // staged bytes of the regular path (a multiple of 1024)
 struct DbpShared {
-  uint8_t stage[kDStage + 16];          // regular path: block headers and bodies
+  uint8_t stage[kDStage + 32];          // regular path: block headers and bodies
   uint8_t win[kWin];
   int64_t body[kBlocks];                // stream offset of the block's first miniblock
   uint64_t mind[kBlocks];               // min delta (as unsigned for wrapping adds)
+  uint64_t wpk[kBlocks];                // staged path: the block's miniblock widths, one per byte
+  uint32_t sbody[kBlocks];              // staged path: stage byte of the block's first miniblock
   uint8_t widths[kBlocks][kMaxMb];
   int64_t mb_off[kBlocks][kMaxMb];      // stream offset of each miniblock
   uint8_t gwidths[256];                 // generic path: miniblock widths of the block
@@ -346,10 +348,115 @@ __device__ __forceinline__ int dbp_decode_rest(gcu8 s, int64_t n, int64_t readab
   return kOK;
 }
 
+// Eight-byte values at base + 8 (4 L + k), k < nv (4 except at the ragged
+// end), as aligned 16-byte granules: base is 8-byte aligned, so the run
+// starts 0 or 8 bytes before a granule; at 8, lane L stores its values 1..3
+// and lane L + 1's value 0 (DPP wave_shl:1), lane 0 its value 0 alone.
+template <bool Full>
+__device__ __forceinline__ void store_run64(uintptr_t base, const uint64_t (&v)[4], int nv) {
+  const int lane = lane_id();
+  const bool shifted = __builtin_amdgcn_readfirstlane((int)(base & 8)) != 0;
+  const uintptr_t o = base + 32 * (uintptr_t)lane;
+  if (!shifted) {
+    if (Full || nv == 4) {
+      stg16(o, make_uint4((uint32_t)v[0], (uint32_t)(v[0] >> 32), (uint32_t)v[1], (uint32_t)(v[1] >> 32)));
+      stg16(o + 16, make_uint4((uint32_t)v[2], (uint32_t)(v[2] >> 32), (uint32_t)v[3], (uint32_t)(v[3] >> 32)));
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (k < nv) stg8(o + 8 * k, (uint32_t)v[k], (uint32_t)(v[k] >> 32));
+    }
+    return;
+  }
+  const uint32_t n0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v[0], 0x130, 0xf, 0xf, true);
+  const uint32_t n1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v[0] >> 32), 0x130, 0xf, 0xf, true);
+  const int nxv = Full ? 4 : __builtin_amdgcn_update_dpp(0, nv, 0x130, 0xf, 0xf, true);
+  if (Full ? lane < 63 : (nv == 4 && nxv >= 1)) {
+    stg16(o + 8, make_uint4((uint32_t)v[1], (uint32_t)(v[1] >> 32), (uint32_t)v[2], (uint32_t)(v[2] >> 32)));
+    stg16(o + 24, make_uint4((uint32_t)v[3], (uint32_t)(v[3] >> 32), n0, n1));
+  } else {
+#pragma unroll
+    for (int k = 1; k < 4; k++)
+      if (k < nv) stg8(o + 8 * k, (uint32_t)v[k], (uint32_t)(v[k] >> 32));
+    if (nxv >= 1 && (Full || nv == 4) && lane < 63) stg8(o + 32, n0, n1);
+  }
+  if (lane == 0 && nv >= 1) stg8(o, (uint32_t)v[0], (uint32_t)(v[0] >> 32));
+}
+
+// One tile of the staged DBP path: positions [t0, t0 + 256) of the batch
+// starting at p0 (4 consecutive positions per lane, all below p_end when
+// Full), unpacked from the stage and prefix-summed on top of carry; returns
+// the value after the tile.
+template <bool Full>
+__device__ __forceinline__ uint64_t dbp_tile(const DbpShared& sh, const PQG_L uint32_t* stw, int64_t t0, int64_t p0,
+                                             int64_t p_end, bool pow2, int bs_sh, int mb_sh, int32_t bs, int32_t mbvc,
+                                             uint64_t carry, bool is64, gu8 out) {
+  const int lane = lane_id();
+  const int64_t pb = t0 + lane * 4;
+  const int nvp = Full ? 4 : (pb >= p_end ? 0 : (p_end - pb >= 4 ? 4 : (int)(p_end - pb)));
+  const uint32_t rl = Full || nvp > 0 ? (uint32_t)(pb - p0) : 0u;  // < kBlocks * bs <= 2^31 (regular)
+  uint32_t b, r2, m, j;
+  if (pow2) {
+    b = rl >> bs_sh;
+    r2 = rl & (uint32_t)(bs - 1);
+    m = r2 >> mb_sh;
+    j = r2 & (uint32_t)(mbvc - 1);
+  } else {
+    b = rl / (uint32_t)bs;
+    r2 = rl - b * (uint32_t)bs;
+    m = r2 / (uint32_t)mbvc;
+    j = r2 - m * (uint32_t)mbvc;
+  }
+  const PQG_L DbpShared* S = lds_ptr(&sh);
+  const uint64_t wpk = S->wpk[b];
+  const int wv = (int)(wpk >> (8 * m)) & 0xff;
+  // bytes of the miniblocks before m: sum of widths below m, times mbvc / 8
+  uint64_t lw = wpk & ((1ull << (8 * m)) - 1);  // m < 8
+  lw = (lw & 0x00ff00ff00ff00ffull) + ((lw >> 8) & 0x00ff00ff00ff00ffull);
+  lw += lw >> 16;
+  lw += lw >> 32;
+  const uint32_t bit0 = (S->sbody[b] + (uint32_t)(mbvc / 8) * ((uint32_t)lw & 0xffff)) * 8 + j * (uint32_t)wv;
+  const uint64_t mnd = S->mind[b];
+  const uint64_t wmask = wv == 64 ? ~0ull : ((1ull << wv) - 1);  // wv == 0: 0
+  uint64_t d[4], local = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t bt = bit0 + (uint32_t)(k * wv);
+    const uint32_t dw = bt >> 5, sh5 = bt & 31;
+    const uint64_t lo = (uint64_t)stw[dw] | ((uint64_t)stw[dw + 1] << 32);
+    const uint64_t x = (lo >> sh5) | (((uint64_t)stw[dw + 2] << (63 - sh5)) << 1);
+    const uint64_t dv = (x & wmask) + mnd;
+    d[k] = Full || k < nvp ? dv : 0;
+    local += d[k];
+  }
+  const uint64_t incl = wave_incl_scan_u64(local);
+  uint64_t run = carry + (incl - local);
+  if (is64) {
+    uint64_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      v[k] = run;
+      run += d[k];
+    }
+    store_run64<Full>((uintptr_t)(out + t0 * 8), v, nvp);
+  } else {
+    uint32_t dw4[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      dw4[k] = (uint32_t)run;
+      run += d[k];
+    }
+    store_run_aligned<4>((uintptr_t)(out + t0 * 4), dw4, nvp);
+  }
+  const uint64_t tot = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)incl, 63) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(incl >> 32), 63) << 32;
+  return carry + tot;
+}
+
 // Values of a DBP page: emulates deltaBitPackDecoder{32,64}.next for positions
 // [0, nn).  Regular layout (miniblock value count a multiple of 8, <= kMaxMb
 // miniblocks): wave-parallel unpack + wrapping scan; otherwise one lane.
-__device__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_t nn, gu8 out,
+__device__ __forceinline__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_t nn, gu8 out,
                           DbpShared& sh, int stage /*0 = header only (read phase), 1 = decode*/) {
   const int lane = lane_id();
   Window win{s, n, kFarAway, lds_ptr(sh.win)};
@@ -366,6 +473,15 @@ __device__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_
   if (mbvc == 0) return kDELTA;
   if ((e = read_u32var_delta(win, pos, &total))) return e;
   if ((e = read_signed(win, pos, is64, &first))) return e;
+  // wave-uniform from here on (scalar registers, uniform branches)
+  bs = __builtin_amdgcn_readfirstlane(bs);
+  mbc = __builtin_amdgcn_readfirstlane(mbc);
+  mbvc = __builtin_amdgcn_readfirstlane(mbvc);
+  total = __builtin_amdgcn_readfirstlane(total);
+  pos = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pos) |
+                  (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)pos >> 32)) << 32);
+  first = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)first) |
+          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(first >> 32)) << 32;
   const int maxw = is64 ? 64 : 32;
   // first readMiniBlockHeader (part of init)
   {
@@ -446,6 +562,10 @@ __device__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_
   int64_t p0 = 0;          // first position of the current batch
   int64_t st_lo = kFarAway, st_hi = kFarAway;  // staged stream range (st_lo: a 16-byte aligned address)
   PQG_L uint8_t* const stb = lds_ptr(sh.stage);
+  const PQG_L uint32_t* const stw = (const PQG_L uint32_t*)stb;
+  const uint64_t wmask_mbc = mbc >= 8 ? ~0ull : (1ull << (8 * mbc)) - 1;
+  const uint64_t wadd = 0x0101010101010101ull * (uint64_t)(127 - maxw);
+  const int32_t mb_bytes_per_w = mbvc / 8;  // bytes of a miniblock per bit of width
   while (p0 < P) {
     int nb = 0;
     int64_t p_end = p0;
@@ -457,38 +577,83 @@ __device__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_
         dbp_restage(s, n, stb, blk_pos, st_lo, st_hi);
         fresh = true;
       }
-      // block header: min delta + widths (readMiniBlockHeader)
-      int64_t hp = blk_pos;
-      uint64_t ux;
-      int ev = dbp_st_uvarint(stb, st_lo, n, hp, &ux);
-      if (ev) return ev == kEOF ? kEOF : kDELTA;
+      // block header (readMiniBlockHeader): its <= 10 varint bytes and <= 8
+      // widths come from one read of 7 stage dwords, made wave-uniform
+      const uint32_t hr = (uint32_t)(blk_pos - st_lo);
+      uint32_t h[7];
+#pragma unroll
+      for (int k = 0; k < 7; k++) h[k] = __builtin_amdgcn_readfirstlane(stw[(hr >> 2) + k]);
+      const uint32_t hs = (hr & 3) * 8;
+      uint64_t x0 = (uint64_t)h[0] | (uint64_t)h[1] << 32, x1 = (uint64_t)h[2] | (uint64_t)h[3] << 32;
+      uint64_t x2 = (uint64_t)h[4] | (uint64_t)h[5] << 32;
+      if (hs) {
+        x0 = (x0 >> hs) | (x1 << (64 - hs));
+        x1 = (x1 >> hs) | (x2 << (64 - hs));
+        x2 = (x2 >> hs) | ((uint64_t)h[6] << (64 - hs));
+      }
+      // binary.ReadUvarint: bytes at or past n are EOF; a terminator after 9
+      // continuation bytes overflows (kDELTA).  Headers of <= 8 bytes (every
+      // int64 delta below 2^55) are decoded branch-free from x0.
+      uint64_t ux = 0;
+      int vl = 0;
+      const uint64_t cont = ~x0 & 0x8080808080808080ull;
+      if (cont) {
+        vl = (int)(__builtin_ctzll(cont) >> 3) + 1;
+        if (blk_pos + vl > n) return kEOF;
+        uint64_t t = x0 & 0x7f7f7f7f7f7f7f7full;
+        t = (t & 0x007f007f007f007full) | ((t & 0x7f007f007f007f00ull) >> 1);
+        t = (t & 0x00003fff00003fffull) | ((t & 0x3fff00003fff0000ull) >> 2);
+        t = (t & 0x000000000fffffffull) | ((t & 0x0fffffff00000000ull) >> 4);
+        ux = vl == 8 ? t : t & ((1ull << (7 * vl)) - 1);
+      } else {
+        for (;; vl++) {
+          if (vl == 10) break;  // >= 10 continuation bytes: the exact walk decides
+          if (blk_pos + vl >= n) return kEOF;
+          const uint32_t bt = (uint32_t)((vl < 8 ? x0 >> (8 * vl) : x1 >> (8 * (vl - 8))) & 0xff);
+          if (bt < 0x80) {
+            if (vl == 9 && bt > 1) return kDELTA;
+            ux |= (uint64_t)bt << (7 * vl);
+            vl++;
+            break;
+          }
+          ux |= (uint64_t)(bt & 0x7f) << (7 * vl);
+        }
+        if (vl == 10 && ((x1 >> 8) & 0x80)) {
+          if (nb > 0) break;
+          return dbp_decode_rest(s, n, readable, is64, nn, out, sh, P, p0, blk_pos, carry, bs, mbc, mbvc, total,
+                                 pow2, bs_sh, mb_sh);
+        }
+      }
       int64_t mdv = (int64_t)(ux >> 1);
       if (ux & 1) mdv = ~mdv;
       if (!is64 && (mdv > 2147483647LL || mdv < -2147483648LL)) return kDELTA;
       const uint64_t md = (uint64_t)mdv;
+      const int64_t hp = blk_pos + vl;
       if (n - hp < mbc) return kEOF;
+      const uint32_t vs = (uint32_t)vl * 8;
+      uint64_t wpk = vs == 0 ? x0 : vs < 64 ? (x0 >> vs) | (x1 << (64 - vs)) : vs == 64 ? x1
+                                                                          : (x1 >> (vs - 64)) | (x2 << (128 - vs));
+      wpk &= wmask_mbc;
+      // a width above maxw (< 128): the byte's top bit, or its low 7 bits + (127 - maxw) carry into it
+      if (((wpk | ((wpk & 0x7f7f7f7f7f7f7f7full) + wadd)) & 0x8080808080808080ull) != 0) return kBIT_WIDTH;
+      uint64_t sw = (wpk & 0x00ff00ff00ff00ffull) + ((wpk >> 8) & 0x00ff00ff00ff00ffull);
+      sw += sw >> 16;
+      sw += sw >> 32;
+      const uint32_t sumw = (uint32_t)sw & 0xffff;
+      const int64_t body = hp + mbc;
+      const int64_t off = body + (int64_t)mb_bytes_per_w * sumw;
       // groups of this block that positions < P read: each must be whole
       const int64_t bp0 = p_end;
       const int64_t bp1 = bp0 + bs < P ? bp0 + bs : P;
-      const int64_t rel = ((bp1 - 1) / 8) * 8 - bp0;  // the last group read
-      const int m_last = (int)(rel / mbvc);
-      const int64_t g_in_mb = (rel % mbvc) / 8;
-      int64_t off = hp + mbc, mo_last = 0;
-      int w_last = 0;
-      for (int m = 0; m < mbc; m++) {
-        const int wv = stb[hp + m - st_lo];
-        if (wv > maxw) return kBIT_WIDTH;
-        if (m == m_last) {
-          w_last = wv;
-          mo_last = off;
-        }
-        if (lane == 0) {
-          sh.widths[nb][m] = (uint8_t)wv;
-          sh.mb_off[nb][m] = off - st_lo;  // stage byte of the miniblock
-        }
-        off += (int64_t)(mbvc / 8) * wv;
+      int64_t g_end = off;
+      if (bp1 - bp0 < bs) {
+        const int64_t rel = ((bp1 - 1) / 8) * 8 - bp0;  // the last group read
+        const int m_last = (int)(rel / mbvc);
+        const int64_t g_in_mb = (rel % mbvc) / 8;
+        int64_t mo = body;
+        for (int m = 0; m < m_last; m++) mo += (int64_t)(mbvc / 8) * ((wpk >> (8 * m)) & 0xff);
+        g_end = mo + (g_in_mb + 1) * (int64_t)((wpk >> (8 * m_last)) & 0xff);
       }
-      const int64_t g_end = mo_last + (g_in_mb + 1) * w_last;
       if (g_end > n) return kEOF;
       if (g_end > st_hi) {  // the block's body is not staged
         if (nb > 0) break;
@@ -498,7 +663,11 @@ __device__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_
         fresh = true;
         continue;
       }
-      if (lane == 0) sh.mind[nb] = md;
+      if (lane == 0) {
+        sh.mind[nb] = md;
+        sh.wpk[nb] = wpk;
+        sh.sbody[nb] = (uint32_t)(body - st_lo);  // stage byte of the first miniblock
+      }
       nb++;
       p_end = bp1;
       blk_pos = off;
@@ -507,66 +676,10 @@ __device__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, bool is64, int64_
     // unpack + wrapping prefix over positions [p0, p_end): value(p) = carry + sum of deltas.
     // A lane's 4 positions share one miniblock (mbvc % 8 == 0): the block /
     // miniblock split once per lane, by shifts for power-of-two sizes.
-    const PQG_L uint32_t* stw = (const PQG_L uint32_t*)stb;
-    for (int64_t t0 = p0; t0 < p_end; t0 += 256) {
-      uint64_t d[4];
-      uint64_t local = 0;
-      const int64_t pb = t0 + lane * 4;
-      const uint32_t rl = (uint32_t)(pb - p0);  // < kBlocks * bs <= 2^31 (regular)
-      uint32_t b, r2, m, j;
-      if (pow2) {
-        b = rl >> bs_sh;
-        r2 = rl & (uint32_t)(bs - 1);
-        m = r2 >> mb_sh;
-        j = r2 & (uint32_t)(mbvc - 1);
-      } else {
-        b = rl / (uint32_t)bs;
-        r2 = rl - b * (uint32_t)bs;
-        m = r2 / (uint32_t)mbvc;
-        j = r2 - m * (uint32_t)mbvc;
-      }
-      const bool any = pb < p_end;
-      const int wv = any ? sh.widths[b][m] : 0;
-      const uint32_t bit0 = any ? (uint32_t)sh.mb_off[b][m] * 8 + j * (uint32_t)wv : 0u;
-      const uint64_t mnd = any ? sh.mind[b] : 0;
-      const uint64_t wmask = wv == 64 ? ~0ull : ((1ull << wv) - 1);
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        uint64_t dv = 0;
-        if (pb + k < p_end) {
-          const uint32_t bt = bit0 + (uint32_t)(k * wv);
-          const uint32_t dw = bt >> 5, sh5 = bt & 31;
-          const uint64_t lo = (uint64_t)stw[dw] | ((uint64_t)stw[dw + 1] << 32);
-          uint64_t x = lo >> sh5;
-          if (sh5 + wv > 64) x |= (uint64_t)stw[dw + 2] << (64 - sh5);
-          dv = (wv ? (x & wmask) : 0) + mnd;
-        }
-        d[k] = dv;
-        local += dv;
-      }
-      uint64_t incl = wave_incl_scan_u64(local);
-      uint64_t run = carry + (incl - local);
-      const int nvp = pb >= p_end ? 0 : (p_end - pb >= 4 ? 4 : (int)(p_end - pb));
-      if (is64) {
-        uint32_t dw8[8];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          dw8[2 * k] = (uint32_t)run;
-          dw8[2 * k + 1] = (uint32_t)(run >> 32);
-          run += d[k];
-        }
-        store_run_aligned<8>((uintptr_t)(out + t0 * 8), dw8, 2 * nvp);
-      } else {
-        uint32_t dw4[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          dw4[k] = (uint32_t)run;
-          run += d[k];
-        }
-        store_run_aligned<4>((uintptr_t)(out + t0 * 4), dw4, nvp);
-      }
-      carry += __shfl(incl, 63, 64);
-    }
+    int64_t t0 = p0;
+    for (; t0 + 256 <= p_end; t0 += 256)
+      carry = dbp_tile<true>(sh, stw, t0, p0, p_end, pow2, bs_sh, mb_sh, bs, mbvc, carry, is64, out);
+    if (t0 < p_end) carry = dbp_tile<false>(sh, stw, t0, p0, p_end, pow2, bs_sh, mb_sh, bs, mbvc, carry, is64, out);
     __builtin_amdgcn_wave_barrier();
     p0 = p_end;
   }
