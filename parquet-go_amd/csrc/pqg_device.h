@@ -308,6 +308,43 @@ __device__ __forceinline__ int64_t wave_min(int64_t v) {
   }
   return v;
 }
+// ---------------------------------------------------------------------------
+// The chain 0 -> next(0) -> ... among 128 speculative positions (next0 /
+// next1: the successor of positions lane / 64 + lane, 128 when it leaves the
+// positions or the item there fails), as two 64-bit masks, by pointer doubling
+// instead of a serial readlane walk: J_k = next^(2^k) by ds_bpermute, then the
+// marks {next^m(0) : m < 64} in six scatter rounds through 128 LDS flag bytes
+// F (k = 5..0).  Items are >= 2 positions long, so the chain has <= 64 of them.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void chain_marks128(int next0, int next1, PQG_L uint8_t* F, uint64_t& cm0, uint64_t& cm1) {
+  const int lane = lane_id();
+  uint32_t j0[6], j1[6];
+  j0[0] = (uint32_t)next0;
+  j1[0] = (uint32_t)next1;
+#pragma unroll
+  for (int k = 1; k < 6; k++) {
+    const uint32_t q0 = j0[k - 1], q1 = j1[k - 1];
+    const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((q0 & 63) * 4), (int)j0[k - 1]);
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((q0 & 63) * 4), (int)j1[k - 1]);
+    const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((q1 & 63) * 4), (int)j0[k - 1]);
+    const uint32_t b1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((q1 & 63) * 4), (int)j1[k - 1]);
+    j0[k] = q0 < 64 ? a0 : q0 < 128u ? b0 : 128u;
+    j1[k] = q1 < 64 ? a1 : q1 < 128u ? b1 : 128u;
+  }
+  F[lane] = lane == 0 ? 1 : 0;
+  F[64 + lane] = 0;
+  cm0 = 1;
+  cm1 = 0;
+#pragma unroll
+  for (int k = 5; k >= 0; k--) {
+    if (((cm0 >> lane) & 1) && j0[k] < 128u) F[j0[k]] = 1;
+    if (((cm1 >> lane) & 1) && j1[k] < 128u) F[j1[k]] = 1;
+    __builtin_amdgcn_wave_barrier();
+    cm0 = __ballot(F[lane] != 0);
+    cm1 = __ballot(F[64 + lane] != 0);
+  }
+}
+
 // inclusive scan of uint64 (wrapping): DPP row_shr 1/2/4/8 then row_bcast
 // 15/31 on both halves, one 64-bit add per step (no LDS round trips)
 __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
@@ -323,14 +360,10 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
   return v;
 }
 __device__ __forceinline__ int64_t wave_excl_scan_i64(int64_t v, int64_t* total) {
-  int l = lane_id();
-  int64_t x = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    int64_t t = __shfl_up(x, o, 64);
-    if (l >= o) x += t;
-  }
-  *total = __shfl(x, 63, 64);
-  return x - v;
+  const uint64_t x = wave_incl_scan_u64((uint64_t)v);  // DPP, wrapping = two's complement
+  *total = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63) |
+                     (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63) << 32);
+  return (int64_t)x - v;
 }
 
 // Block-wide exclusive scan (NT threads, NT/64 waves); `part` holds NT/64+1

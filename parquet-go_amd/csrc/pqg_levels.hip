@@ -566,43 +566,6 @@ struct LevelDecoder {
     __builtin_amdgcn_wave_barrier();
   }
 
-  // The chain of true run headers among the window's kLPos speculative
-  // positions (next0 / next1: the next header of positions lane / 64 + lane,
-  // kLPos when it leaves the window or the header fails), by pointer doubling
-  // instead of a serial walk: J_k = next^(2^k) by ds_bpermute, then the marks
-  // {next^m(0) : m < 64} in six scatter rounds through LDS flags (k = 5..0).
-  // Every header that does not fail is >= 2 bytes (a header byte plus an RLE
-  // value byte or >= 1 bit-packed group), so the chain has <= 64 runs.
-  __device__ __forceinline__ void chain_marks(int next0, int next1, uint64_t& cm0, uint64_t& cm1) {
-    const int lane = lane_id();
-    uint32_t j0[6], j1[6];
-    j0[0] = (uint32_t)next0;
-    j1[0] = (uint32_t)next1;
-#pragma unroll
-    for (int k = 1; k < 6; k++) {
-      const uint32_t q0 = j0[k - 1], q1 = j1[k - 1];
-      const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((q0 & 63) * 4), (int)j0[k - 1]);
-      const uint32_t b0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((q0 & 63) * 4), (int)j1[k - 1]);
-      const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((q1 & 63) * 4), (int)j0[k - 1]);
-      const uint32_t b1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((q1 & 63) * 4), (int)j1[k - 1]);
-      j0[k] = q0 < 64 ? a0 : q0 < (uint32_t)kLPos ? b0 : (uint32_t)kLPos;
-      j1[k] = q1 < 64 ? a1 : q1 < (uint32_t)kLPos ? b1 : (uint32_t)kLPos;
-    }
-    PQG_L uint8_t* F = lds_ptr(sh->cflag);
-    F[lane] = lane == 0 ? 1 : 0;
-    F[64 + lane] = 0;
-    cm0 = 1;
-    cm1 = 0;
-#pragma unroll
-    for (int k = 5; k >= 0; k--) {
-      if (((cm0 >> lane) & 1) && j0[k] < (uint32_t)kLPos) F[j0[k]] = 1;
-      if (((cm1 >> lane) & 1) && j1[k] < (uint32_t)kLPos) F[j1[k]] = 1;
-      __builtin_amdgcn_wave_barrier();
-      cm0 = __ballot(F[lane] != 0);
-      cm1 = __ballot(F[64 + lane] != 0);
-    }
-  }
-
   // decode `count` values; kOK or the stream's first error
   __device__ int run() {
     const int lane = lane_id();
@@ -644,7 +607,7 @@ struct LevelDecoder {
         pp = __builtin_amdgcn_readlane(n1, pp - 64);
       }
 #else
-      chain_marks(n0, n1, cm0, cm1);
+      chain_marks128(n0, n1, lds_ptr(sh->cflag), cm0, cm1);
 #endif
       const bool on0 = (cm0 >> lane) & 1, on1 = (cm1 >> lane) & 1;
       PQG_LT(tc);

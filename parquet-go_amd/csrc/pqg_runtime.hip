@@ -489,7 +489,7 @@ static int launch_pipeline(pqg_ctx* c) {
                      (const int*)c->idx2slot.p, (const int*)c->ok2slot.p, (int*)c->order.p);
   hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n);
   if (c->timed) hipEventRecord(c->ev[1], s);
-  hipLaunchKernelGGL(k_page_list, dim3(n), dim3(256), 0, s, jobs, pages, n, list,
+  hipLaunchKernelGGL(k_page_list, dim3(n), dim3(1024), 0, s, jobs, pages, n, list,
                      (int)std::min<int64_t>(c->list_cap, INT32_MAX), ctr, ctr + 8);
   if (c->timed) hipEventRecord(c->ev[2], s);
   bool any_comp = false;

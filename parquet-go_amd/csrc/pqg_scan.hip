@@ -737,15 +737,15 @@ __global__ void __launch_bounds__(64) k_scan_pages(JobDev* jobs, PageDev* pages,
 // ============================================================================
 // K1f: compact list of page indices over all jobs.
 // ============================================================================
-// One 256-lane block per job: the job's pages in the list (at the offset of
+// One 1024-lane block per job: the job's pages in the list (at the offset of
 // the pages of the jobs before it), and each data page's region of the value
 // stream's run table / block index — an exclusive scan of a bound from the
 // page's sizes (the same bound reg_stream used to take with two contended
 // atomics per page): a value stream of B bytes and n values has at most
 // B/2 + 2 runs and n/kHBlock + runs/kHBlockRuns + B/(kHBlockBytes/2) + 3 blocks.
-__global__ void __launch_bounds__(256) k_page_list(JobDev* jobs, PageDev* pages, int n_jobs, int* list, int list_cap,
-                                                   int* total, int* queues) {
-  __shared__ int64_t part[5];
+__global__ void __launch_bounds__(1024) k_page_list(JobDev* jobs, PageDev* pages, int n_jobs, int* list, int list_cap,
+                                                    int* total, int* queues) {
+  __shared__ int64_t part[17];
   __shared__ int s_off;
   const int j = blockIdx.x;
   auto pages_of = [&](int i) {
@@ -769,7 +769,7 @@ __global__ void __launch_bounds__(256) k_page_list(JobDev* jobs, PageDev* pages,
   JobDev& job = jobs[j];
   const int n = pages_of(j);
   int64_t rc = 0, bc = 0;
-  for (int b = 0; b < n; b += 256) {
+  for (int b = 0; b < n; b += 1024) {
     const int i = b + threadIdx.x;
     int64_t nr = 0, nb = 0;
     if (i < n) {
@@ -782,8 +782,8 @@ __global__ void __launch_bounds__(256) k_page_list(JobDev* jobs, PageDev* pages,
       }
     }
     int64_t tr, tb;
-    const int64_t er = block_excl_scan<256>(nr, &tr, part);
-    const int64_t eb = block_excl_scan<256>(nb, &tb, part);
+    const int64_t er = block_excl_scan<1024>(nr, &tr, part);
+    const int64_t eb = block_excl_scan<1024>(nb, &tb, part);
     if (i < n) {
       pages[job.page_base + i].run_off = rc + er;
       pages[job.page_base + i].blk_off = bc + eb;

@@ -51,14 +51,14 @@ int prof_read_snappy(unsigned long long* out) {
 // ============================================================================
 constexpr int kPos = 128;         // tag positions parsed per window (2 per lane)
 #ifndef PQG_SNAPPY_DENSE
-#define PQG_SNAPPY_DENSE 4
+#define PQG_SNAPPY_DENSE 8
 #endif
 constexpr int kDense = PQG_SNAPPY_DENSE;  // tags in a window for the batched byte resolution
 constexpr int kSnWin = 4096;      // compressed-stream window (LDS)
 constexpr int kSnWinNeed = 2048;  // window bytes wanted ahead of the first tag
 constexpr int kSpan = 1024;       // output bytes a batch covers: 64 lanes x one 16-byte granule
 #ifndef PQG_SNAPPY_RING
-#define PQG_SNAPPY_RING 16384
+#define PQG_SNAPPY_RING 8192
 #endif
 constexpr int kRing = PQG_SNAPPY_RING;  // output history kept in LDS (a power of two)
 // flush granularity (a wave's stores are waited for at the next loop head);
@@ -75,6 +75,7 @@ struct SnapShared {
   uint8_t tmap[kSpan];    // 1 + tag position, at the tag's first output byte
   u32x2_t tent[kPos];     // per tag position: {output start (relative to the batch's first granule),
                           //  literal: 0x80000000 | window offset of its bytes; copy: offset}
+  uint8_t cflag[kPos];    // chain marks of the pointer-doubling walk
 };
 
 // ---- 64-lane DPP scans (row_shr 1/2/4/8, row_bcast 15/31)
@@ -515,23 +516,19 @@ struct SnapBlock {
       const Tag t1 = parse_tag(IN, wo + 64, s + 64 + lane, slen, 64 + lane);
       const int n0 = (t0.err || t0.next >= kPos) ? kPos : (int)t0.next;
       const int n1 = (t1.err || t1.next >= kPos) ? kPos : (int)t1.next;
-      // ---- 2. the chain, one v_readlane per tag
-      uint64_t cm0 = 0, cm1 = 0;
-      int p = 0, last = 0;
-      const int64_t lim64 = slen - s;  // tags start before the end of the block
+      // ---- 2. the chain (pointer doubling, pqg_device.h); tags start before
+      // the end of the block
+      uint64_t cm0, cm1;
+      chain_marks128(n0, n1, lds_ptr(sh->cflag), cm0, cm1);
+      const int64_t lim64 = slen - s;
       const int lim = lim64 < kPos ? (int)lim64 : kPos;
-      // one tight loop per half (a bit set, a readlane, a compare per tag)
-      const int lim0 = lim < 64 ? lim : 64;
-      while (p < lim0) {
-        last = p;
-        cm0 |= 1ull << p;
-        p = __builtin_amdgcn_readlane(n0, p);
+      if (lim < 64) {
+        cm0 &= (1ull << lim) - 1;
+        cm1 = 0;
+      } else if (lim < kPos) {
+        cm1 &= (1ull << (lim - 64)) - 1;
       }
-      while (p < lim) {
-        last = p;
-        cm1 |= 1ull << (p - 64);
-        p = __builtin_amdgcn_readlane(n1, p - 64);
-      }
+      const int last = cm1 ? 127 - __builtin_clzll(cm1) : 63 - __builtin_clzll(cm0);
       const bool on0 = (cm0 >> lane) & 1, on1 = (cm1 >> lane) & 1;
       PQG_ST(tc);
       PQG_SA(1, tc - tb);
