@@ -355,8 +355,8 @@ class FileReader:
     """Mirror of parquet-go's FileReader (file_reader.go:27-118): the selected
     columns of a file (dotted paths, schema.isSelected schema.go:296-312; none =
     all), decoded one row group at a time on the GPU.  `source` is the file's
-    bytes or a path; each row group uploads only its selected chunks' byte span
-    (span_jobs)."""
+    bytes or a path (then only the footer and the selected chunks are read);
+    each row group uploads only its selected chunks' bytes (span_jobs)."""
 
     def __init__(self, source, *columns, device=0, decoder=None):
         self.file = ParquetFile.open(source) if isinstance(source, (str, os.PathLike)) else ParquetFile(source)
