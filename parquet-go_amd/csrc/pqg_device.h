@@ -289,8 +289,11 @@ __device__ __forceinline__ int queue_pull(int* queue) {
 // scalar loads, which do not queue behind vector loads and stores (vmcnt) the
 // way vector loads of the same fields would.
 __device__ __forceinline__ int queue_next(int* queue) {
+  // the first active lane pulls: should a compiler ever make the caller's loop
+  // divergent, the active lanes still agree on t (no lane re-reads a stale 0)
+  const int leader = __builtin_amdgcn_readfirstlane(lane_id());
   int t = 0;
-  if (lane_id() == 0) t = queue_pull(queue);
+  if (lane_id() == leader) t = queue_pull(queue);
   return __builtin_amdgcn_readfirstlane(t);
 }
 

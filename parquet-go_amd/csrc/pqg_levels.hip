@@ -987,15 +987,15 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
 
 // ---- K3d ---------------------------------------------------------------------
 // notNull prefix per chunk + dictionary-page resolution; one 256-lane block per job.
-__global__ void __launch_bounds__(256) k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch) {
-  __shared__ int64_t part[5];
+__global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch) {
+  __shared__ int64_t part[17];
   JobDev& job = jobs[blockIdx.x];
   int np = job.num_pages < job.page_cap ? job.num_pages : job.page_cap;
   if (job.status == kCAPACITY) np = 0;
   // each thread takes a contiguous segment of pages: its loads are
-  // independent (one round trip per pass, not one per 256 pages), one block
+  // independent (one round trip per pass, not one per 1024 pages), one block
   // scan of the segment sums, then the offsets are written in a second pass
-  const int seg = (np + 255) / 256;
+  const int seg = (np + 1023) / 1024;
   const int s0 = (int)threadIdx.x * seg, s1 = s0 + seg < np ? s0 + seg : np;
   PageDev* pp = pages + job.page_base;
   auto nn_of = [&](int i) -> int64_t {
@@ -1006,7 +1006,7 @@ __global__ void __launch_bounds__(256) k_nn_scan(JobDev* jobs, PageDev* pages, u
 #pragma unroll 8
   for (int i = s0; i < s1; i++) sum += nn_of(i);
   int64_t carry;
-  int64_t run = block_excl_scan<256>(sum, &carry, part);
+  int64_t run = block_excl_scan<1024>(sum, &carry, part);
 #pragma unroll 8
   for (int i = s0; i < s1; i++) {
     pp[i].value_offset = run;

@@ -512,7 +512,7 @@ static int launch_pipeline(pqg_ctx* c) {
   hipLaunchKernelGGL(k_hybrid_walk, dim3(walk_blocks), dim3(kWalkLanes), 0, s, pages, list, ctr, streams, runs, blks);
   if (c->timed) hipEventRecord(c->ev[5], s);
   if (c->timed) hipEventRecord(c->ev[6], s);
-  hipLaunchKernelGGL(k_nn_scan, dim3(n), dim3(256), 0, s, jobs, pages, scratch);
+  hipLaunchKernelGGL(k_nn_scan, dim3(n), dim3(1024), 0, s, jobs, pages, scratch);
   if (c->timed) hipEventRecord(c->ev[7], s);
   // every values kernel takes the whole page list and keeps the pages whose
   // vmode (set by k_page_levels) is its own
@@ -547,7 +547,7 @@ static int launch_pipeline(pqg_ctx* c) {
                        Q(kQueueStrDba), (uint8_t*)c->value_arena.p, offs);
   }
   if (c->timed) hipEventRecord(c->ev[9], s);
-  hipLaunchKernelGGL(k_finalize, dim3(n), dim3(256), 0, s, jobs, n, pages);
+  hipLaunchKernelGGL(k_finalize, dim3(n), dim3(1024), 0, s, jobs, n, pages);
   if (c->timed) hipEventRecord(c->ev[10], s);
   return hip_ok(hipGetLastError());
 }

@@ -190,7 +190,10 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, int from_lane) {
 // position >= hi inside them, which points at itself) and the output bytes on
 // the way, so every chain in the window advances past it at once.
 // ---------------------------------------------------------------------------
-__device__ void chain_walk(gcu8 src, int64_t slen, int64_t hi, int64_t& x, uint32_t& acc) {
+// RD: the 8 bytes at block offset p -> (lo, hi) (global memory, or a segment
+// staged in LDS by k_snap_seg)
+template <class RD>
+__device__ void chain_walk_rd(const RD& rd, int64_t slen, int64_t hi, int64_t& x, uint32_t& acc) {
   const int lane = lane_id();
   for (;;) {
     const bool act = x < hi;
@@ -204,7 +207,7 @@ __device__ void chain_walk(gcu8 src, int64_t slen, int64_t hi, int64_t& x, uint3
     const int64_t wb = (int64_t)__builtin_amdgcn_readfirstlane(xm);
     const int64_t p = wb + lane;
     uint32_t lo, hw;
-    ld8_block(src, slen, p, lo, hw);
+    rd(p, lo, hw);
     const Tag t = parse_tag_bytes(lo, hw, p, slen, lane);
     uint32_t J = t.next < 0x7fffffff ? (uint32_t)t.next : 0x7fffffffu;  // relative to wb
     uint32_t O = t.len < (1 << 30) ? (uint32_t)t.len : (1u << 30);
@@ -229,6 +232,27 @@ __device__ void chain_walk(gcu8 src, int64_t slen, int64_t hi, int64_t& x, uint3
       acc = sat_add(acc, Ox);
     }
   }
+}
+struct GlobalRd8 {
+  gcu8 src;
+  int64_t slen;
+  __device__ __forceinline__ void operator()(int64_t p, uint32_t& lo, uint32_t& hi) const { ld8_block(src, slen, p, lo, hi); }
+};
+// bytes of a segment staged in LDS from block offset st_lo (16-byte aligned in
+// memory); every position the walk of [b, hi) reads, < hi + 72, is staged
+struct LdsRd8 {
+  const PQG_L uint8_t* st;
+  int64_t st_lo;
+  __device__ __forceinline__ void operator()(int64_t p, uint32_t& lo, uint32_t& hi) const {
+    const uint32_t o = (uint32_t)(p - st_lo);
+    const PQG_L uint32_t* q = (const PQG_L uint32_t*)(st + (o & ~3u));
+    const uint32_t a = q[0], b = q[1], c = q[2], sft = (o & 3) * 8;
+    lo = __builtin_amdgcn_alignbit(b, a, sft);
+    hi = __builtin_amdgcn_alignbit(c, b, sft);
+  }
+};
+__device__ void chain_walk(gcu8 src, int64_t slen, int64_t hi, int64_t& x, uint32_t& acc) {
+  chain_walk_rd(GlobalRd8{src, slen}, slen, hi, x, acc);
 }
 
 struct SnapBlock {
@@ -900,6 +924,8 @@ __global__ void __launch_bounds__(256) k_snap_plan(const JobDev* jobs, PageDev* 
 // first 64 bytes unless a literal longer than that ends inside it.
 __global__ void __launch_bounds__(64) k_snap_seg(const JobDev* jobs, const PageDev* pages, const int* seg_page,
                                                  const int* seg_total, int seg_cap, uint2* F) {
+  constexpr int kStG = (kSnapSeg + 16 + 72 + 1023) / 1024;  // staged KiB: the segment, its alignment, the read-ahead
+  __shared__ __attribute__((aligned(16))) uint8_t st[kStG * 1024 + 16];
   const int lane = lane_id();
   const int n = min(*seg_total, seg_cap);
   for (int g = blockIdx.x; g < n; g += gridDim.x) {
@@ -909,10 +935,25 @@ __global__ void __launch_bounds__(64) k_snap_seg(const JobDev* jobs, const PageD
     const SnapLoc L = snap_loc(pg);
     const int64_t b = pg.sn_hdr + (int64_t)(g - pg.sn_seg_base) * kSnapSeg;
     const int64_t hi = b + kSnapSeg < L.clen ? b + kSnapSeg : L.clen;
+    const gcu8 src = gconst(job.data) + L.src_off;
+    // the segment in LDS with one round of loads (granules holding a block
+    // byte are mapped; the others read as zero)
+    const int64_t st_lo = b - (int64_t)(((uintptr_t)(src + b)) & 15);
+    uint4 v[kStG];
+#pragma unroll
+    for (int k = 0; k < kStG; k++) {
+      const int64_t o = st_lo + 16 * (int64_t)(lane + 64 * k);
+      v[k] = (o < L.clen && o + 16 > 0) ? ldg16((uintptr_t)(src + o)) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < kStG; k++) sts16(lds_ptr(st) + 16 * (lane + 64 * k), v[k]);
+    __builtin_amdgcn_wave_barrier();
     int64_t x = b + lane;
     uint32_t acc = 0;
-    chain_walk(gconst(job.data) + L.src_off, L.clen, hi, x, acc);
+    chain_walk_rd(LdsRd8{lds_ptr(st), st_lo}, L.clen, hi, x, acc);
     F[(int64_t)g * 64 + lane] = make_uint2(x < 0x7fffffff ? (uint32_t)x : 0x7fffffffu, acc);
+    __builtin_amdgcn_wave_barrier();
   }
 }
 

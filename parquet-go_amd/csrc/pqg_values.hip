@@ -826,7 +826,7 @@ template __global__ void k_values<3>(JobDev*, PageDev*, const int*, const int*, 
 // K5: chunk status in reference order (readPages errors first, then
 // readPageData errors) — one 256-lane block per job, min-reductions over pages.
 // ============================================================================
-__global__ void __launch_bounds__(256) k_finalize(JobDev* jobs, int n_jobs, PageDev* pages) {
+__global__ void __launch_bounds__(1024) k_finalize(JobDev* jobs, int n_jobs, PageDev* pages) {
   __shared__ int s_read, s_dec;
   JobDev& job = jobs[blockIdx.x];
   if (job.status == kCAPACITY) return;
@@ -839,7 +839,7 @@ __global__ void __launch_bounds__(256) k_finalize(JobDev* jobs, int n_jobs, Page
   const PageDev* pg = pages + job.page_base;
   int r = INT32_MAX, d = INT32_MAX;
 #pragma unroll 8
-  for (int i = threadIdx.x; i < np; i += 256) {
+  for (int i = threadIdx.x; i < np; i += 1024) {
     if (pg[i].read_status != kOK && i < r) r = i;
     if ((pg[i].page_type == 0 || pg[i].page_type == 3) && pg[i].decode_status != kOK && i < d) d = i;
   }
