@@ -199,12 +199,17 @@ __device__ void chain_walk_rd(const RD& rd, int64_t slen, int64_t hi, int64_t& x
     const bool act = x < hi;
     if (!__ballot(act)) break;
     uint32_t xm = act ? (uint32_t)x : 0xffffffffu;  // block offsets are < 2^31
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const uint32_t y = (uint32_t)__shfl_xor((int)xm, o, 64);
-      xm = y < xm ? y : xm;
+    // wave minimum by DPP (row_shr 1/2/4/8, row_bcast 15/31; lanes without a
+    // source keep the identity), read from lane 63: no LDS round trips
+#define PQG_MIN_STEP(ctrl, rm)                                                                          \
+    {                                                                                                   \
+      const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffffu, (int)xm, ctrl, rm, 0xf, false); \
+      xm = y < xm ? y : xm;                                                                             \
     }
-    const int64_t wb = (int64_t)__builtin_amdgcn_readfirstlane(xm);
+    PQG_MIN_STEP(0x111, 0xf) PQG_MIN_STEP(0x112, 0xf) PQG_MIN_STEP(0x114, 0xf) PQG_MIN_STEP(0x118, 0xf)
+    PQG_MIN_STEP(0x142, 0xa) PQG_MIN_STEP(0x143, 0xc)
+#undef PQG_MIN_STEP
+    const int64_t wb = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)xm, 63);
     const int64_t p = wb + lane;
     uint32_t lo, hw;
     rd(p, lo, hw);
