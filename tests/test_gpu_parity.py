@@ -1,8 +1,10 @@
 """GPU parity: libpqgpu (HIP, gfx950) vs the CPU oracle, bit-exact, through the C ABI.
 
 Sizes here are small enough for the oracle to finish in seconds; the
-full-size configs are checked by bench.py's verify pass and by
-size-independent properties (test_gpu_properties.py).
+full-size configs are checked by bench.py's verify pass against the
+generator's own arrays (`verified_bit_exact`), and cases larger than the
+kernels' LDS windows (long runs, >= 1 MiB snappy pages, long DBA values) by
+test_levels.py, test_snappy_split.py and test_delta_strings.py.
 """
 import json
 import os
