@@ -7,10 +7,11 @@ file, ~10% nulls, RLE_DICTIONARY with D = 2^b entries for every index width b in
 20 000 rows per page.  A step decodes all seven column chunks (700M slots) in
 one batched call, inputs resident in HBM.
 
-Sub-results (same line, "configs"): C1 (required int64 PLAIN, 10M rows), C3
-(int64 DELTA_BINARY_PACKED, V2, SNAPPY, 200M rows), C4 (STRING dictionary +
-PLAIN fallback, SNAPPY, 50M rows) and one C5 shard (8 row groups x 15.625M rows
-of LIST<double> + 8 mixed columns).  Each carries its own roofline (dominant
+Sub-results (same line, "configs"): C1 (required int64 PLAIN, 10M rows) and
+its one-page variant (the reference writer's layout), C2 run-heavy (index runs
+of geometric length, mean 16), C3 (int64 DELTA_BINARY_PACKED, V2, SNAPPY, 200M
+rows), C4 (STRING dictionary + PLAIN fallback, SNAPPY, 50M rows) and one C5
+shard (8 row groups x 15.625M rows of LIST<double> + 8 mixed columns).  Each carries its own roofline (dominant
 stage + whole pipeline) and CPU baseline.
 
 Multi-GPU (one process per GPU, weak scaling): the data set has 8N C5 row
@@ -50,11 +51,19 @@ def log(*a):
 
 
 def host_cores():
+    """Host threads for the all-cores CPU baseline: the process's CPU affinity,
+    capped by the harness's per-GPU CPU share when one is declared (the GPU box
+    sets OMP_NUM_THREADS=16 per GPU while sched_getaffinity shows every CPU of
+    the machine).  Returns (threads, note)."""
     try:
-        n = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(n, 16))  # the GPU box grants 16 host threads per GPU
+        aff = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and 0 < int(share) < aff:
+        return int(share), "sched_getaffinity %d CPUs; capped at the box's per-GPU share OMP_NUM_THREADS=%s" % (
+            aff, share)
+    return max(1, aff), "sched_getaffinity %d CPUs" % aff
 
 
 # ---------------------------------------------------------------- workloads
@@ -73,19 +82,26 @@ def gen_workload(key, args, rank, world):
     from pqgpu import shard
     t0 = time.time()
     files = []
-    if key == "c2":
+    if key in ("c2", "c2_run_heavy"):
+        rh = key == "c2_run_heavy"
         rgs = list(shard.row_groups_for_rank(world, rank, world))  # N row groups per width
         bits_list = [int(b) for b in args.bits.split(",")]
         for rg in rgs:
-            for bits, data, exp in W.config_c2_family(rows=args.rows, bits_list=bits_list, seed=2 + rg):
+            for bits, data, exp in W.config_c2_family(rows=args.rows, bits_list=bits_list, seed=2 + rg,
+                                                      run_heavy=rh):
                 files.append((pqgpu.ParquetFile(data), [(0, 0)], ("c2", exp)))
-        desc = ("C2: optional INT32, %d rows x %d dictionary widths (b=%s), ~10%% nulls, RLE_DICTIONARY, V1, "
-                "UNCOMPRESSED, 20000 rows/page" % (args.rows, len(bits_list), args.bits))
+        desc = ("C2%s: optional INT32, %d rows x %d dictionary widths (b=%s), ~10%% nulls, RLE_DICTIONARY (%s), V1, "
+                "UNCOMPRESSED, 20000 rows/page" % (" run-heavy" if rh else "", args.rows, len(bits_list), args.bits,
+                                                  "index runs of geometric length, mean 16" if rh
+                                                  else "uniform indices"))
         dtype = "int32"
-    elif key == "c1":
-        data, info = W.config_c1(rows=args.c1_rows)
+    elif key in ("c1", "c1_1page"):
+        one = key == "c1_1page"
+        data, info = W.config_c1(rows=args.c1_rows, rows_per_page=args.c1_rows if one else 20000)
         files.append((pqgpu.ParquetFile(data), [(0, 0)], ("flat", [info["values"]])))
-        desc = "C1: required INT64, %d rows, PLAIN, UNCOMPRESSED, 1 RG, V1, 20000 rows/page" % args.c1_rows
+        desc = ("C1: required INT64, %d rows, PLAIN, UNCOMPRESSED, 1 RG, V1, %s" % (
+            args.c1_rows, "ONE data page (parquet-go's writer layout, chunk_writer.go:237-246)" if one
+            else "20000 rows/page"))
         dtype = "int64"
     elif key == "c3":
         data, info = W.config_c3(rows=args.c3_rows)
@@ -106,7 +122,9 @@ def gen_workload(key, args, rank, world):
         pf = pqgpu.ParquetFile(data)
         files.append((pf, [(i, c) for i in range(len(rgs)) for c in range(pf.num_columns)], ("c5", info)))
         desc = ("C5 shard: row groups %s of %d (RG i -> GPU floor(i*%d/%d)), %d rows each: LIST<double> + int32, "
-                "int64 DBP, double, float, int96, optional int32 dict, string dict, int64 SNAPPY"
+                "int64 DBP, double, float, int96, optional int32 (PLAIN), string dict, int64 SNAPPY; the columns with "
+                "nulls or a dictionary (LIST, optional int32, string) one data page per chunk with one bit-packed "
+                "run per level/index stream (parquet-go's writer layout: quirk-free), the others 20000 rows/page"
                 % (rgs, R, world, R, args.c5_rows_per_rg))
         dtype = "mixed"
     else:
@@ -211,28 +229,21 @@ def verify(wl, dec, res):
 # ---------------------------------------------------------------- CPU baseline
 def cpu_baseline(wl, seconds):
     """The oracle (C++ restatement of parquet-go's readPages/readPageData) on a
-    bounded sample of the workload's chunks: one thread (parquet-go's one
-    goroutine per FileReader, file_reader.go:27-118), then the same sample split
-    into page ranges over a pool of the host's threads (pages decode
-    independently once the dictionary is read; ctypes releases the GIL)."""
+    bounded sample of the workload's chunks.  Both legs run the SAME tasks —
+    each sampled chunk cut into page ranges (pqo_decode_page_range: the
+    dictionary page, then the range's pages decoded and their outputs
+    materialised) — once on one thread (parquet-go's one goroutine per
+    FileReader, file_reader.go:27-118) and once over a pool of the host's
+    threads (pages decode independently once the dictionary is read; ctypes
+    releases the GIL), so the ratio is a true speed-up."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import pyoracle as O
-    from pqgpu import abi
     OL = O.lib()
     jobs = []
     for pf, specs, _ in wl.files:
         for (rg, col) in specs:
             jobs.append(pf.host_job(rg, col)[0])
-
-    def run(job):
-        r = abi.ChunkResult()
-        pages = (abi.PageInfo * 1)()
-        n = C.c_int(0)
-        OL.pqo_decode_chunk(C.byref(job), C.byref(r), pages, 1, C.byref(n))
-        lev = r.num_slots * ((job.col.max_def > 0) + (job.col.max_rep > 0))
-        b = lev + (r.num_values * r.value_width if r.value_width else r.values_bytes + (r.num_values + 1) * 4)
-        OL.pqo_free_result(C.byref(r))
-        return b
+    cores, note = host_cores()
 
     def run_range(task):
         job, lo, hi = task
@@ -241,31 +252,32 @@ def cpu_baseline(wl, seconds):
         assert rc >= 0, rc
         return b.value
 
-    done, t1, k = 0, 0.0, 0
+    def ranges(job):  # ~4 ranges per pool thread over the chunk's pages
+        n = int(OL.pqo_decode_page_range(C.byref(job), 0, 0, None))
+        per = max(1, -(-n // (4 * cores)))
+        return [(job, lo, min(n, lo + per)) for lo in range(0, n, per)]
+
+    done, t1, k, tasks = 0, 0.0, 0, []
     while k < len(jobs) and t1 < seconds / 2:
+        tk = ranges(jobs[k])
         t = time.perf_counter()
-        done += run(jobs[k])
+        done += sum(run_range(x) for x in tk)
         t1 += time.perf_counter() - t
+        tasks += tk
         k += 1
     single = done / t1 / 1e9
-    cores = host_cores()
-    # the same k chunks, as page ranges: ~4 ranges per thread over all pages
-    tasks = []
-    for job in jobs[:k]:
-        n = int(OL.pqo_decode_page_range(C.byref(job), 0, 0, None))
-        per = max(1, -(-n // max(1, (4 * cores) // k)))
-        tasks += [(job, lo, min(n, lo + per)) for lo in range(0, n, per)]
     t = time.perf_counter()
     with ThreadPoolExecutor(max_workers=cores) as ex:
         pool_bytes = sum(ex.map(run_range, tasks))
     tp = time.perf_counter() - t
+    assert pool_bytes == done
     return ({"value": round(single, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-             "sample": "oracle (C++ restatement of parquet-go readPages/readPageData) on %d of %d chunks, one thread "
-                       "like parquet-go's one-goroutine FileReader; %.1fs" % (k, len(jobs), t1)},
+             "sample": "oracle (C++ restatement of parquet-go readPages/readPageData) on %d of %d chunks as %d page "
+                       "ranges run in turn on one thread, like parquet-go's one-goroutine FileReader; %.1fs"
+                       % (k, len(jobs), len(tasks), t1)},
             {"value": round(pool_bytes / tp / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": "port",
-             "sample": "oracle on the same %d chunks split into %d page ranges over a pool of %d host threads "
-                       "(pages decode independently once the dictionary is read); %.1fs"
-                       % (k, len(tasks), cores, tp)})
+             "speedup": round(t1 / tp, 2), "cores_note": note,
+             "sample": "the same %d page ranges over a pool of %d host threads; %.1fs" % (len(tasks), cores, tp)})
 
 
 # ---------------------------------------------------------------- PMC traffic (committed passes)
@@ -386,16 +398,23 @@ def k8_c2(dec, wl, res, args):
     a, vb, sb, _ = dec.assemble(r.def_levels, r.rep_levels, r.values, r.num_slots, 1, 0, 4,
                                 validity=True, spaced=True, offsets=False)
     reps = 5
-    t1 = time.perf_counter()
+    ms, host_ms = 0.0, 0.0
+    dm = C.c_float()
     for _ in range(reps):
+        t1 = time.perf_counter()
         rc = L.pqg_assemble(dec.ctx, C.byref(a))
+        host_ms += (time.perf_counter() - t1) * 1e3
         assert rc == 0, abi.status_name(rc)
-    ms = (time.perf_counter() - t1) / reps * 1e3
+        L.pqg_last_assemble_ms(dec.ctx, C.byref(dm))
+        ms += dm.value
+    ms /= reps
     n = r.num_slots
     nbytes = n + r.num_values * 4 + n * 4 + (n + 7) // 8
     out = {"kernels": "k_asm_count+k_asm_scan+k_asm_write<4>", "slots": n, "ms": round(ms, 4), "alg_bytes": nbytes,
            "achieved_GBs": round(nbytes / (ms * 1e-3) / 1e9, 1),
-           "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "timer": "host wall, incl. sync"}
+           "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "timer": "HIP events on the decode stream around the K8 kernels (pqg_last_assemble_ms)",
+           "host_ms_incl_sync": round(host_ms / reps, 4)}
     if not args.no_verify:
         defs, vals = wl.files[0][2][1]
         valid = defs == 1
@@ -418,10 +437,11 @@ def k8_list_c5(dec, wl, res, args):
     for i in idx:
         r = res[i]
         a, lvp, lop, evp, vvp = dec.assemble_list(r.def_levels, r.rep_levels, r.values, r.num_slots, 3, 1, 2, 8)
-        t1 = time.perf_counter()
         rc = L.pqg_assemble_list(dec.ctx, C.byref(a))
         assert rc == 0, abi.status_name(rc)
-        tot_ms += (time.perf_counter() - t1) * 1e3
+        dm = C.c_float()
+        L.pqg_last_assemble_ms(dec.ctx, C.byref(dm))
+        tot_ms += dm.value
         n = r.num_slots
         tot_bytes += 2 * n + r.num_values * 8 + (a.num_rows + 1) * 4 + (a.num_rows + 7) // 8 + \
             (a.num_elements + 7) // 8 + a.num_elements * 8
@@ -437,7 +457,8 @@ def k8_list_c5(dec, wl, res, args):
             dec.free(p)
     out = {"kernels": "k_list_count+k_list_scan+k_list_write<8>", "chunks": len(idx), "ms": round(tot_ms, 4),
            "alg_bytes": tot_bytes, "achieved_GBs": round(tot_bytes / (tot_ms * 1e-3) / 1e9, 1),
-           "frac": round(tot_bytes / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "timer": "host wall, incl. sync"}
+           "frac": round(tot_bytes / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "timer": "HIP events on the decode stream around the K8 kernels (pqg_last_assemble_ms)"}
     if not args.no_verify:
         out["verified"] = bool(ok)
     return out
@@ -466,7 +487,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=100_000_000, help="C2 rows per file")
     ap.add_argument("--bits", type=str, default="1,2,4,8,12,16,20")
-    ap.add_argument("--configs", type=str, default="c1,c3,c4,c5", help="sub-results besides the C2 headline")
+    ap.add_argument("--configs", type=str, default="c1,c1_1page,c2_run_heavy,c3,c4,c5",
+                    help="sub-results besides the C2 headline")
     ap.add_argument("--sub-steps", type=int, default=5)
     ap.add_argument("--c1-rows", type=int, default=10_000_000)
     ap.add_argument("--c3-rows", type=int, default=200_000_000)

@@ -101,7 +101,20 @@ void bitpack(Buf& b, const uint64_t* v, int64_t n, int w) {
 // RLE / bit-packing hybrid encoder: literal groups of 8 aligned to the start
 // of the literal segment; a run of >= min_rle equal values starting at an
 // aligned position becomes an RLE run; literal runs <= 64 groups.
+// max_groups < 0: parquet-go's own hybridEncoder (hybrid_encoder.go:59-99):
+// the whole stream is ONE bit-packed run (bpEncode: header (groups << 1) | 1,
+// the values padded to a multiple of 8), nothing for a zero width.
 void hybrid_encode(Buf& out, const uint32_t* v, int64_t n, int w, int min_rle = 8, int max_groups = 64) {
+  if (max_groups < 0) {
+    if (w == 0 || n == 0) return;
+    const int64_t groups = (n + 7) / 8;
+    put_uvarint(out, (uint64_t)(groups << 1 | 1));
+    std::vector<uint64_t> tmp((size_t)(groups * 8), 0);
+    for (int64_t k = 0; k < n; k++) tmp[(size_t)k] = v[k];
+    bitpack(out, tmp.data(), groups * 8, w);
+    return;
+  }
+  if (max_groups == 0) max_groups = 64;
   if (w == 0) {  // one RLE run without value bytes (readers other than parquet-go read it)
     if (n > 0) put_uvarint(out, (uint64_t)n << 1);
     return;
@@ -314,6 +327,7 @@ struct ColSpec {
   int64_t num_slots, num_values;
   int min_rle;
   int v2_uncompressed_flag;  // write is_compressed=false on V2 pages (Q4 probe)
+  int hybrid_groups;         // literal groups per bit-packed run (0: 64; < 0: one run per stream, parquet-go's writer)
 };
 
 int type_width(int type, int tl) {
@@ -488,18 +502,18 @@ ChunkOut write_chunk(Buf& file, const ColSpec& c, int64_t s0, int64_t s1, int64_
     if (maxr > 0) {
       lv.assign((size_t)n, 0);
       for (int64_t i = 0; i < n; i++) lv[(size_t)i] = c.rep_levels[ps + i];
-      hybrid_encode(rep, lv.data(), n, rw, c.min_rle);
+      hybrid_encode(rep, lv.data(), n, rw, c.min_rle, c.hybrid_groups);
     }
     if (maxd > 0) {
       lv.assign((size_t)n, 0);
       for (int64_t i = 0; i < n; i++) lv[(size_t)i] = c.def_levels[ps + i];
-      hybrid_encode(def, lv.data(), n, dw, c.min_rle);
+      hybrid_encode(def, lv.data(), n, dw, c.min_rle, c.hybrid_groups);
     }
     int enc = c.encoding;
     if (enc == 8 && (!use_dict || ve > dict_values_end)) enc = 0;  // PLAIN fallback
     if (enc == 8) {
       vals.push_back((uint8_t)idx_w);
-      hybrid_encode(vals, idx.data() + (vs - v0), nn, idx_w, c.min_rle);
+      hybrid_encode(vals, idx.data() + (vs - v0), nn, idx_w, c.min_rle, c.hybrid_groups);
       any_dict = true;
     } else if (enc == 6 || enc == 7) {
       delta_byte_array(vals, c.values, c.offsets, vs, ve, enc == 7);
@@ -563,7 +577,7 @@ extern "C" {
 typedef struct pqw_column {
   const char* name;
   int32_t type, type_length, repetition, encoding, codec, page_version, rows_per_page, min_rle;
-  int32_t v2_uncompressed_flag, reserved;
+  int32_t v2_uncompressed_flag, hybrid_groups;
   int64_t dict_limit;
   const uint8_t* values;
   const int64_t* offsets;
@@ -603,6 +617,7 @@ int pqw_write_file(const pqw_column* cols, int ncols, int64_t num_rows, int row_
     c.num_values = p.num_values;
     c.min_rle = p.min_rle > 0 ? p.min_rle : 8;
     c.v2_uncompressed_flag = p.v2_uncompressed_flag;
+    c.hybrid_groups = p.hybrid_groups;
     int maxd = c.repetition == 0 ? 0 : (c.repetition == 1 ? 1 : 3);
     auto& rs = row_start_slots[(size_t)k];
     for (int64_t i = 0; i < c.num_slots; i++)

@@ -16,6 +16,7 @@ PLAIN, RLE_DICTIONARY, DELTA_BINARY_PACKED = 0, 8, 5
 DELTA_LENGTH_BYTE_ARRAY, DELTA_BYTE_ARRAY = 6, 7
 UNCOMPRESSED, SNAPPY = 0, 1
 REQUIRED, OPTIONAL, LIST = 0, 1, 2
+REF_HYBRID = -1  # Column(hybrid_groups=...): parquet-go's writer layout (one bit-packed run per stream)
 
 _lib = None
 
@@ -26,7 +27,7 @@ class _PqwColumn(C.Structure):
         ("type", C.c_int32), ("type_length", C.c_int32), ("repetition", C.c_int32),
         ("encoding", C.c_int32), ("codec", C.c_int32), ("page_version", C.c_int32),
         ("rows_per_page", C.c_int32), ("min_rle", C.c_int32),
-        ("v2_uncompressed_flag", C.c_int32), ("reserved", C.c_int32),
+        ("v2_uncompressed_flag", C.c_int32), ("hybrid_groups", C.c_int32),
         ("dict_limit", C.c_int64),
         ("values", C.c_void_p), ("offsets", C.c_void_p),
         ("def_levels", C.c_void_p), ("rep_levels", C.c_void_p),
@@ -61,7 +62,8 @@ def lib():
 class Column:
     def __init__(self, name, ptype, values, *, type_length=0, repetition=REQUIRED, encoding=PLAIN,
                  codec=UNCOMPRESSED, page_version=1, rows_per_page=20000, def_levels=None,
-                 rep_levels=None, offsets=None, dict_limit=0, min_rle=8, v2_uncompressed_flag=False):
+                 rep_levels=None, offsets=None, dict_limit=0, min_rle=8, v2_uncompressed_flag=False,
+                 hybrid_groups=0):
         self.name = name
         self.ptype = ptype
         self.type_length = type_length
@@ -73,6 +75,10 @@ class Column:
         self.min_rle = min_rle
         self.dict_limit = dict_limit
         self.v2_uncompressed_flag = v2_uncompressed_flag
+        # literal groups per bit-packed run of the level / index streams: 0 = 64
+        # (pyarrow-like); REF_HYBRID = one bit-packed run per stream, as
+        # parquet-go's hybridEncoder writes them (hybrid_encoder.go:59-99)
+        self.hybrid_groups = hybrid_groups
         self.values = np.ascontiguousarray(values)
         self.offsets = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.int64)
         self.def_levels = None if def_levels is None else np.ascontiguousarray(def_levels, dtype=np.uint8)
@@ -108,6 +114,7 @@ def write_file(columns, num_rows, row_groups=1):
         a.encoding, a.codec, a.page_version = c.encoding, c.codec, c.page_version
         a.rows_per_page, a.min_rle = c.rows_per_page, c.min_rle
         a.v2_uncompressed_flag = int(c.v2_uncompressed_flag)
+        a.hybrid_groups = c.hybrid_groups
         a.dict_limit = c.dict_limit
         a.values = c.values.ctypes.data if c.values.size else None
         a.offsets = c.offsets.ctypes.data if c.offsets is not None else None
@@ -290,14 +297,23 @@ def config_delta_strings(rows=200_000, encoding=DELTA_BYTE_ARRAY, rows_per_page=
 
 
 def config_c2_family(rows=100_000_000, bits_list=(1, 2, 4, 8, 12, 16, 20), null_frac=0.10, rows_per_page=20000,
-                     seed=2):
+                     seed=2, run_heavy=False):
     """C2 at every index width: one file per width sharing the null pattern and
-    the (masked) uniform index draw.  Yields (bits, file_bytes, expected) where
-    expected = (def_levels u8[rows], dense int32 values)."""
+    the (masked) index draw.  Index streams: uniform keys
+    (bit-packed dominated), or run_heavy: keys repeated in runs of geometric
+    length, mean 16 (RLE runs dominate).  Yields (bits, file_bytes, expected)
+    where expected = (def_levels u8[rows], dense int32 values)."""
     rng = np.random.default_rng(seed)
     defs = (rng.random(rows) >= null_frac).astype(np.uint8)
     nn = int(defs.sum())
-    raw = rng.integers(0, 1 << 20, size=nn, dtype=np.int64)
+    if run_heavy:
+        lens = rng.geometric(1.0 / 16, size=nn // 8 + 64)
+        while int(lens.sum()) < nn:
+            lens = np.concatenate([lens, rng.geometric(1.0 / 16, size=nn // 16 + 64)])
+        keys = rng.integers(0, 1 << 20, size=len(lens), dtype=np.int64)
+        raw = np.repeat(keys, lens)[:nn]
+    else:
+        raw = rng.integers(0, 1 << 20, size=nn, dtype=np.int64)
     dict_all = rng.integers(-2**31, 2**31 - 1, size=1 << 20, dtype=np.int64).astype(np.int32)
     for bits in bits_list:
         d = 1 << bits
@@ -392,23 +408,30 @@ def config_c5(row_groups=(0,), rows_per_rg=C5_ROWS_PER_RG, seed=5, rows_per_page
 
     rows = rows_per_rg * len(parts)
     rpp_d = _dbp_safe_rows_per_page(rows_per_rg, rows_per_page)
+    # Quirk-free by construction: the reference appends each page's
+    # whole numValues-long slice to the column store, trailing nils included
+    # (Q1, chunk_reader.go:394-397), and from the second row group on decodes a
+    # dictionary page into the store's reused backing array, which the first
+    # data page's append then overwrites (Q2, chunk_reader.go:235,
+    # page_dict.go:50-53).  Both need a chunk with more than one data page, so
+    # every column with nulls (lst, oi32) or a dictionary (s) is written the way
+    # parquet-go's own writer writes every chunk: ONE data page per chunk
+    # (chunk_writer.go:237-246), its level and index streams one bit-packed run
+    # each (hybridEncoder.bpEncode, hybrid_encoder.go:59-73).  The columns
+    # without nulls keep pyarrow's 20 000 rows per page.
+    one = dict(rows_per_page=rows_per_rg, hybrid_groups=REF_HYBRID)
     cols = [
         Column("lst", DOUBLE, cat("lst", "values"), repetition=LIST, def_levels=cat("lst", "def_levels"),
-               rep_levels=cat("lst", "rep_levels"), rows_per_page=rows_per_page),
+               rep_levels=cat("lst", "rep_levels"), **one),
         Column("i32", INT32, cat("i32", "values"), rows_per_page=rows_per_page),
         Column("i64d", INT64, cat("i64d", "values"), encoding=DELTA_BINARY_PACKED, rows_per_page=rpp_d),
         Column("f64", DOUBLE, cat("f64", "values"), rows_per_page=rows_per_page),
         Column("f32", FLOAT, cat("f32", "values"), rows_per_page=rows_per_page),
         Column("i96", INT96, cat("i96", "values"), rows_per_page=rows_per_page),
-        # the optional int32 column is written with dictionary off
-        # (PLAIN) so that no quirk triggers: Q1 (per-page trailing nils,
-        # chunk_reader.go:394-397) and Q2 (dictionary aliasing of the reused
-        # values array from row group 2 on, chunk_reader.go:235) both need a
-        # multi-page dictionary chunk with nulls
+        # the optional int32 column is written with dictionary off (PLAIN)
         Column("oi32", INT32, cat("oi32", "values"), repetition=OPTIONAL, encoding=PLAIN,
-               def_levels=cat("oi32", "def_levels"), rows_per_page=rows_per_page),
-        Column("s", BYTE_ARRAY, cat("s", "values"), offsets=cat("s", "offsets"), encoding=RLE_DICTIONARY,
-               rows_per_page=rows_per_page),
+               def_levels=cat("oi32", "def_levels"), **one),
+        Column("s", BYTE_ARRAY, cat("s", "values"), offsets=cat("s", "offsets"), encoding=RLE_DICTIONARY, **one),
         Column("i64s", INT64, cat("i64s", "values"), codec=SNAPPY, rows_per_page=rows_per_page),
     ]
     data = write_file(cols, rows, row_groups=len(parts))

@@ -357,6 +357,11 @@ typedef struct pqg_list_args {
  * PQG_ERR_INVALID_ARG when elements exceed int32 offsets. */
 int pqg_assemble_list(pqg_ctx* ctx, pqg_list_args* args);
 
+/* Device time (ms) of the K8 kernels of the last pqg_assemble /
+ * pqg_assemble_list call: HIP events on the ctx stream around its kernel
+ * launches (the count read-back and host syncs excluded). */
+int pqg_last_assemble_ms(pqg_ctx* ctx, float* ms);
+
 /* ---- host-side planner: footer / schema (file_meta.go:14-62, schema.go) --- */
 typedef struct pqg_file pqg_file;
 
@@ -390,6 +395,7 @@ void pqg_file_close(pqg_file* f);
 int pqg_file_num_columns(const pqg_file* f);
 int pqg_file_num_row_groups(const pqg_file* f);
 int64_t pqg_file_num_rows(const pqg_file* f);
+/* PQG_ERR_METADATA when the column's dotted path does not fit pqg_column_info.path */
 int pqg_file_column(const pqg_file* f, int col, pqg_column_info* out);
 int pqg_file_chunk(const pqg_file* f, int row_group, int col, pqg_chunk_meta* out);
 int64_t pqg_file_row_group_rows(const pqg_file* f, int row_group);
@@ -407,6 +413,8 @@ typedef struct pqg_schema_node {
   int32_t reserved;
 } pqg_schema_node;
 int pqg_file_num_schema_nodes(const pqg_file* f);
+/* PQG_ERR_METADATA when the node's name does not fit pqg_schema_node.name (a
+ * truncated name would be a different map key than the reference's) */
 int pqg_file_schema_node(const pqg_file* f, int i, pqg_schema_node* out);
 
 /* ======================= oracle (TEST INFRASTRUCTURE) ===================== */
@@ -421,21 +429,24 @@ int pqo_hybrid_decode(const uint8_t* buf, int64_t len, int width, int64_t count,
 int pqo_snappy_decode(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int64_t* out_len);
 int pqo_delta_decode64(const uint8_t* buf, int64_t len, int64_t count, int64_t* out);
 int pqo_delta_decode32(const uint8_t* buf, int64_t len, int64_t count, int32_t* out);
-/* Reference column-store contents (triage of Q1/Q2; fixed-width columns):
- * decode the chunks of one column over `n_row_groups` consecutive row groups
- * the way readRowGroup fills ColumnStore.values (readPageData
- * chunk_reader.go:380-402), with the quirks in `quirks` reproduced
- * (Q2 requires Q1, as in the reference).  Per row group: `entries` store
- * slots, `values` entries x value_width bytes (a nil slot is zeros),
- * `nil_flags` one byte per entry.  Q2 follows Go 1.13's slice growth
- * (runtime growslice + malloc size classes) for []interface{}: outside
- * /root/reference, stated in the oracle, so parity for it is unpinned. */
+/* Reference column-store contents (triage of Q1/Q2): decode the chunks of one
+ * column over `n_row_groups` consecutive row groups the way readRowGroup fills
+ * ColumnStore.values (readPageData chunk_reader.go:380-402), with the quirks in
+ * `quirks` reproduced (Q2 requires Q1, as in the reference).  Per row group:
+ * `entries` store slots, `nil_flags` one byte per entry; fixed width:
+ * `values` entries x value_width bytes (a nil slot is zeros); byte arrays
+ * (value_width 0): `values` the entries' bytes back to back (`chars` of them)
+ * and `offsets[entries + 1]` (a nil entry is empty).  Q2 follows Go 1.13's
+ * slice growth (runtime growslice + malloc size classes) for []interface{}:
+ * outside /root/reference, stated in the oracle, so parity for it is unpinned. */
 typedef struct pqo_store_rg {
   int32_t status;
   int32_t value_width;
   int64_t entries;
   uint8_t* values;
   uint8_t* nil_flags;
+  int64_t* offsets;
+  int64_t chars;
 } pqo_store_rg;
 int pqo_decode_column_store(const pqg_chunk_job* jobs, int n_row_groups, int quirks, pqo_store_rg* out);
 void pqo_free_store(pqo_store_rg* out, int n_row_groups);

@@ -21,7 +21,8 @@ _lib = None
 class StoreRG(C.Structure):
     """pqo_store_rg (include/pqgpu.h)."""
     _fields_ = [("status", C.c_int32), ("value_width", C.c_int32), ("entries", C.c_int64),
-                ("values", C.c_void_p), ("nil_flags", C.c_void_p)]
+                ("values", C.c_void_p), ("nil_flags", C.c_void_p), ("offsets", C.c_void_p),
+                ("chars", C.c_int64)]
 
 
 def lib():
@@ -172,7 +173,9 @@ def assemble_list(def_levels, rep_levels, values, max_def, list_def, elem_def, v
 
 def decode_column_store(jobs, quirks):
     """The reference's ColumnStore.values contents per row group (Q1/Q2 triage):
-    list of (status, values bytes (entries x width), nil flags u8)."""
+    list of (status, values, nil flags u8) where values are the entries' bytes
+    (entries x width) for fixed-width columns and (chars, offsets[entries + 1])
+    for byte arrays."""
     n = len(jobs)
     arr = (abi.ChunkJob * max(n, 1))(*jobs)
     out = (StoreRG * max(n, 1))()
@@ -185,9 +188,15 @@ def decode_column_store(jobs, quirks):
             res.append((o.status, None, None))
             continue
         cnt = o.entries
-        vals = np.ctypeslib.as_array(C.cast(o.values, C.POINTER(C.c_uint8)), shape=(max(cnt * o.value_width, 1),))
-        nil = np.ctypeslib.as_array(C.cast(o.nil_flags, C.POINTER(C.c_uint8)), shape=(max(cnt, 1),))
-        res.append((0, vals[:cnt * o.value_width].copy(), nil[:cnt].copy()))
+        nil = np.ctypeslib.as_array(C.cast(o.nil_flags, C.POINTER(C.c_uint8)), shape=(max(cnt, 1),))[:cnt].copy()
+        if o.value_width > 0:
+            vals = np.ctypeslib.as_array(C.cast(o.values, C.POINTER(C.c_uint8)),
+                                         shape=(max(cnt * o.value_width, 1),))[:cnt * o.value_width].copy()
+        else:
+            chars = np.ctypeslib.as_array(C.cast(o.values, C.POINTER(C.c_uint8)), shape=(max(o.chars, 1),))
+            offs = np.ctypeslib.as_array(C.cast(o.offsets, C.POINTER(C.c_int64)), shape=(cnt + 1,))
+            vals = (chars[:o.chars].copy(), offs.copy())
+        res.append((0, vals, nil))
     lib().pqo_free_store(out, n)
     return res
 

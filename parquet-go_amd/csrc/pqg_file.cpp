@@ -332,6 +332,8 @@ int pqg_file_schema_node(const pqg_file* f, int i, pqg_schema_node* out) {
   if (!f || !out || i < 0 || i >= (int)f->nodes.size()) return PQG_ERR_INVALID_ARG;
   memset(out, 0, sizeof(*out));
   const SNode& n = f->nodes[(size_t)i];
+  // the name is the row's map key (Column.name): never hand out a truncated one
+  if (n.name.size() >= sizeof(out->name)) return PQG_ERR_METADATA;
   snprintf(out->name, sizeof(out->name), "%s", n.name.c_str());
   out->repetition = n.rep;
   out->num_children = n.num_children;
@@ -344,6 +346,7 @@ int pqg_file_schema_node(const pqg_file* f, int i, pqg_schema_node* out) {
 int pqg_file_column(const pqg_file* f, int col, pqg_column_info* out) {
   if (!f || !out || col < 0 || col >= (int)f->leaves.size()) return PQG_ERR_INVALID_ARG;
   memset(out, 0, sizeof(*out));
+  if (f->leaves[(size_t)col].path.size() >= sizeof(out->path)) return PQG_ERR_METADATA;  // no truncated paths
   out->desc = f->leaves[(size_t)col].desc;
   strncpy(out->path, f->leaves[(size_t)col].path.c_str(), sizeof(out->path) - 1);
   return PQG_OK;

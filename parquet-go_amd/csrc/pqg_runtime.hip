@@ -189,6 +189,8 @@ struct pqg_ctx {
   int n_jobs = 0;
   int64_t list_cap = 0;
   hipEvent_t ev[kStages + 1];
+  hipEvent_t ev_k8[4];   // K8: [0,1] assemble / list count, [2,3] list write
+  float k8_ms = 0.f;     // device time of the last pqg_assemble / pqg_assemble_list
   bool timed = true;
 };
 
@@ -235,6 +237,7 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
     return PQG_ERR_HIP;
   }
   for (auto& e : c->ev) hipEventCreate(&e);
+  for (auto& e : c->ev_k8) hipEventCreate(&e);
   if (const char* e = getenv("PQG_DICT4")) c->dict4 = atoi(e) != 0;
   {
     hipFuncAttributes fa;
@@ -264,6 +267,7 @@ void pqg_ctx_destroy(pqg_ctx* c) {
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   for (auto& e : c->ev) hipEventDestroy(e);
+  for (auto& e : c->ev_k8) hipEventDestroy(e);
   for (DevBuf* b : {&c->jobs, &c->pages, &c->list, &c->counters, &c->def_arena, &c->rep_arena, &c->value_arena,
                     &c->scratch, &c->streams, &c->runs, &c->blks, &c->cand_list, &c->vlists, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
                     &c->ok2slot, &c->order, &c->asm_seg, &c->offs_arena, &c->doffs_arena, &c->page_stage,
@@ -651,12 +655,15 @@ int pqg_assemble(pqg_ctx* c, pqg_assemble_args* a) {
   if (c->asm_seg.grow((size_t)(2 * nseg + 2) * sizeof(int64_t))) return PQG_ERR_HIP;
   int64_t* seg = (int64_t*)c->asm_seg.p;
   int64_t* tot = seg + 2 * nseg;
+  hipEventRecord(c->ev_k8[0], c->stream);
   int e = pqg::assemble_launch(c->stream, a, seg, tot);
   if (e) return e;
+  hipEventRecord(c->ev_k8[1], c->stream);
   int64_t h[2] = {0, 0};
   if (hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return PQG_ERR_HIP;
+  hipEventElapsedTime(&c->k8_ms, c->ev_k8[0], c->ev_k8[1]);
   a->num_valid = h[0];
   a->null_count = a->num_slots - h[0];
   a->num_boundaries = h[1];
@@ -672,8 +679,10 @@ int pqg_assemble_list(pqg_ctx* c, pqg_list_args* a) {
   if (c->asm_seg.grow((size_t)(4 * nseg + 4) * sizeof(int64_t))) return PQG_ERR_HIP;
   int64_t* seg = (int64_t*)c->asm_seg.p;
   int64_t* tot = seg + 4 * nseg;
+  hipEventRecord(c->ev_k8[0], c->stream);
   int e = pqg::list_count_launch(c->stream, a, seg, tot);
   if (e) return e;
+  hipEventRecord(c->ev_k8[1], c->stream);
   int64_t h[4] = {0, 0, 0, 0};
   if (hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
@@ -684,9 +693,22 @@ int pqg_assemble_list(pqg_ctx* c, pqg_list_args* a) {
   a->null_lists = h[3];
   // int32 offsets cannot hold the elements: fail before any output is written
   if (h[1] > INT32_MAX) return PQG_ERR_INVALID_ARG;
+  hipEventRecord(c->ev_k8[2], c->stream);
   e = pqg::list_write_launch(c->stream, a, seg);
   if (e) return e;
-  return hip_ok(hipStreamSynchronize(c->stream));
+  hipEventRecord(c->ev_k8[3], c->stream);
+  e = hip_ok(hipStreamSynchronize(c->stream));
+  float m0 = 0.f, m1 = 0.f;
+  hipEventElapsedTime(&m0, c->ev_k8[0], c->ev_k8[1]);
+  hipEventElapsedTime(&m1, c->ev_k8[2], c->ev_k8[3]);
+  c->k8_ms = m0 + m1;
+  return e;
+}
+
+int pqg_last_assemble_ms(pqg_ctx* c, float* ms) {
+  if (!c || !ms) return PQG_ERR_INVALID_ARG;
+  *ms = c->k8_ms;
+  return PQG_OK;
 }
 
 int pqg_decode_chunks(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs, pqg_chunk_result* results) {

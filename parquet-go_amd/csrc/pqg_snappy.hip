@@ -907,6 +907,9 @@ __global__ void __launch_bounds__(256) k_snap_plan(const JobDev* jobs, PageDev* 
       if (split && (sb + nsub > sub_cap || gb + nseg > seg_cap)) {
         split = false;
         fb = 1;  // tables full: the serial path
+        // the slots this page was given that exist: marked empty, so that
+        // k_snap_decode (which reads every slot < min(total, cap)) skips them
+        for (int j = 0; j < nsub && sb + j < sub_cap; j++) subs[sb + j] = SnapSub{pidx, j, -1, 0};
       }
       if (split) {
         for (int j = 0; j < nsub; j++) subs[sb + j] = SnapSub{pidx, j, j == 0 ? hdr : -1, 0};

@@ -40,6 +40,7 @@ def lib():
         "pqg_bench_decode": ([P, C.POINTER(abi.ChunkJob), I, I, C.POINTER(C.c_float), C.POINTER(C.c_float), I], I),
         "pqg_assemble": ([P, C.POINTER(abi.AssembleArgs)], I),
         "pqg_assemble_list": ([P, C.POINTER(abi.ListArgs)], I),
+        "pqg_last_assemble_ms": ([P, C.POINTER(C.c_float)], I),
         "pqg_decode_page": ([P, C.POINTER(abi.PageJob), C.POINTER(abi.ChunkResult)], I),
         "pqg_block_decompress": ([P, I, C.c_char_p, I64, P, I64, C.POINTER(I64)], I),
         "pqg_pack_levels": ([P, P, I64, I, P], I),
@@ -67,7 +68,7 @@ EXPORTED = [
     "pqg_ctx_create", "pqg_ctx_destroy", "pqg_status_string", "pqg_device_alloc", "pqg_device_free",
     "pqg_memcpy_h2d", "pqg_memcpy_d2h", "pqg_decode_chunks_async", "pqg_sync", "pqg_decode_chunks",
     "pqg_get_pages", "pqg_last_timings", "pqg_debug_job", "pqg_debug_counters", "pqg_bench_decode", "pqg_assemble",
-    "pqg_assemble_list", "pqg_decode_page", "pqg_block_decompress", "pqg_pack_levels", "pqg_file_open", "pqg_file_open_tail",
+    "pqg_assemble_list", "pqg_last_assemble_ms", "pqg_decode_page", "pqg_block_decompress", "pqg_pack_levels", "pqg_file_open", "pqg_file_open_tail",
     "pqg_file_close",
     "pqg_file_num_columns", "pqg_file_num_row_groups", "pqg_file_num_rows", "pqg_file_row_group_rows",
     "pqg_file_column", "pqg_file_chunk", "pqg_file_num_schema_nodes", "pqg_file_schema_node",

@@ -121,9 +121,9 @@ class ParquetFile:
         if self.path is None:
             job.data = self._buf.ctypes.data + start
             job.data_len = self.size - start
-        else:  # the chunk's own bytes, kept alive with the file object
+        else:  # the chunk's own bytes, kept alive by the job (not the file)
             b = np.ascontiguousarray(self.read_range(start, start + m.total_compressed_size))
-            self._keep = getattr(self, "_keep", []) + [b]
+            job._keep = b
             job.data = b.ctypes.data if b.nbytes else None
             job.data_len = b.nbytes
         job.total_compressed_size = m.total_compressed_size
@@ -298,13 +298,15 @@ def chunk_span(pf: ParquetFile, specs):
     return max(0, lo), min(hi, pf.size), metas
 
 
-def chunk_ranges(pf: ParquetFile, specs):
+def chunk_ranges(pf: ParquetFile, specs, to_eof=()):
     """The byte ranges the chunks of (rg, col) pairs occupy ([start, start +
-    TotalCompressedSize) each, clipped to the file), sorted, with overlapping or
-    adjacent ranges merged: [(lo, hi)], and the chunks' ChunkMetas."""
+    TotalCompressedSize) each, clipped to the file; [start, end of file) for the
+    spec indices in `to_eof`), sorted, with overlapping or adjacent ranges
+    merged: [(lo, hi)], and the chunks' ChunkMetas."""
     metas = [pf.chunk_meta(rg, c) for rg, c in specs]
-    rs = sorted((max(0, min(m.start, pf.size)), max(0, min(m.start + m.total_compressed_size, pf.size)))
-                for m in metas)
+    rs = sorted((max(0, min(m.start, pf.size)),
+                 pf.size if i in to_eof else max(0, min(m.start + m.total_compressed_size, pf.size)))
+                for i, m in enumerate(metas))
     out = []
     for lo, hi in rs:
         if out and lo <= out[-1][1]:
@@ -314,15 +316,18 @@ def chunk_ranges(pf: ParquetFile, specs):
     return [tuple(r) for r in out], metas
 
 
-def span_jobs(pf: ParquetFile, specs, dec):
+def span_jobs(pf: ParquetFile, specs, dec, to_eof=()):
     """Chunk jobs for (rg, col) pairs with only their chunks' bytes uploaded,
     packed into one device buffer (merged ranges, chunk_ranges), each job
     pointing into it.  Unselected chunks are never read, as skipChunk seeks past
     them (chunk_reader.go:286-312).  A job's readable bytes run to the end of
-    its merged range, which holds all of [start, start + TotalCompressedSize)
-    that the file holds, so min(TotalCompressedSize, data_len) is what the
-    reference would read.  Returns (jobs, device pointer, bytes uploaded)."""
-    ranges, metas = chunk_ranges(pf, specs)
+    its merged range.  That range holds every page HEADER readPages reads (it
+    reads headers while TotalCompressedSize - Count() > 0, chunk_reader.go:212-
+    217), but the reference then reads the whole page from the file, so a last
+    page overrunning an understated TotalCompressedSize needs bytes past it:
+    decode_spans re-uploads such chunks to the end of the file (`to_eof`).
+    Returns (jobs, device pointer, bytes uploaded)."""
+    ranges, metas = chunk_ranges(pf, specs, to_eof)
     total = sum(hi - lo for lo, hi in ranges)
     host = np.empty(max(total, 1), dtype=np.uint8)
     base = []  # packed offset of each range
@@ -349,6 +354,30 @@ def span_jobs(pf: ParquetFile, specs, dec):
         job.data_len = hi - start
         jobs.append(job)
     return jobs, dev, total
+
+
+def decode_spans(pf: ParquetFile, specs, dec):
+    """span_jobs + pqg_decode_chunks for (rg, col) pairs.  A chunk whose decode
+    ends in EOF / size mismatch while the file holds bytes past its uploaded
+    range (a page overrunning TotalCompressedSize, which the reference still
+    reads whole: chunk_reader.go:212-280) is decoded again with the bytes to the
+    end of the file, in a second batched call (device outputs are only valid
+    until the next decode on `dec`).  Returns (results, device buffer, bytes
+    uploaded); the caller frees the buffer after using the outputs."""
+    jobs, dev, nbytes = span_jobs(pf, specs, dec)
+    res = dec.decode_jobs(jobs)
+    retry = set()
+    for i, (job, r) in enumerate(zip(jobs, res)):
+        m = pf.chunk_meta(*specs[i])
+        start = max(0, min(m.start, pf.size))
+        if r.status in (abi.STATUS_CODES["EOF"], abi.STATUS_CODES["SIZE"]) and job.data_len < pf.size - start:
+            retry.add(i)
+    if retry:
+        dec.free(dev)
+        jobs, dev, nb2 = span_jobs(pf, specs, dec, to_eof=retry)
+        nbytes += nb2
+        res = dec.decode_jobs(jobs)
+    return res, dev, nbytes
 
 
 class FileReader:
@@ -389,12 +418,9 @@ class FileReader:
         specs = [(rg, c) for rg in rgs for c in self.selected]
         if not specs:
             return []
-        jobs, dev, nbytes = span_jobs(self.file, specs, self.dec)
+        res, dev, nbytes = decode_spans(self.file, specs, self.dec)
         self.uploaded_bytes += nbytes
-        try:
-            res = self.dec.decode_jobs(jobs)
-        finally:
-            self.dec.free(dev)
+        self.dec.free(dev)
         return [(rg, c, r) for (rg, c), r in zip(specs, res)]
 
     def read_row_group(self, rg):
@@ -402,10 +428,9 @@ class FileReader:
         specs = [(rg, c) for c in self.selected]
         if not specs:
             return {}
-        jobs, dev, nbytes = span_jobs(self.file, specs, self.dec)
+        res, dev, nbytes = decode_spans(self.file, specs, self.dec)
         self.uploaded_bytes += nbytes
         try:
-            res = self.dec.decode_jobs(jobs)
             return {self.file.columns[c].path.decode(): self.dec.download(r, i)
                     for i, ((_, c), r) in enumerate(zip(specs, res))}
         finally:
@@ -424,10 +449,9 @@ class FileReader:
         specs = [(rg, c) for c in self.selected]
         if not specs:
             return {}
-        jobs, dev, nbytes = span_jobs(self.file, specs, self.dec)
+        res, dev, nbytes = decode_spans(self.file, specs, self.dec)
         self.uploaded_bytes += nbytes
         try:
-            res = self.dec.decode_jobs(jobs)
             return {c: self.dec.download(r, i) for i, ((_, c), r) in enumerate(zip(specs, res))}
         finally:
             self.dec.free(dev)

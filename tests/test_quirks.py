@@ -127,3 +127,84 @@ def test_go_size_classes_sample(size, exp):
         pytest.skip("not exported")
     L.pqo_go_roundupsize.restype = C.c_int64
     assert L.pqo_go_roundupsize(C.c_int64(size)) == exp
+
+
+def _store_equal(a, b):
+    assert a[0] == b[0] == 0
+    assert np.array_equal(a[2], b[2])
+    if isinstance(a[1], tuple):
+        assert np.array_equal(a[1][0], b[1][0]) and np.array_equal(a[1][1], b[1][1])
+    else:
+        assert np.array_equal(a[1], b[1])
+
+
+def _store_reads_equal(spec, quirky):
+    """What ColumnStore.get pops (data_store.go:158-203: the next store entry
+    for each slot with dLevel == maxD, in order) is the same: the quirky store
+    starts with the spec store's entries, and Q1's page-tail nils (one page:
+    only at the chunk's end) are never reached."""
+    assert spec[0] == quirky[0] == 0
+    n = len(spec[2])
+    assert not spec[2].any()
+    assert np.array_equal(quirky[2][:n], spec[2]) and quirky[2][n:].all()
+    if isinstance(spec[1], tuple):
+        (c0, o0), (c1, o1) = spec[1], quirky[1]
+        assert np.array_equal(o1[:n + 1], o0) and np.array_equal(c1[:o0[-1]], c0)
+    else:
+        w = len(spec[1]) // max(n, 1)
+        assert np.array_equal(quirky[1][:n * w], spec[1])
+
+
+def test_c5_fixture_is_quirk_free():
+    """the C5 fixture must not trigger Q1/Q2, so that page-level
+    parity (GPU == oracle) is also parity with parquet-go's own NextRow.  Every
+    chunk with nulls or a dictionary has exactly one data page (the layout of
+    parquet-go's writer, chunk_writer.go:237-246), and the reference's
+    column-store contents with Q1|Q2 reproduced equal the spec decode over
+    three row groups in what ColumnStore.get reads, for every column (byte
+    arrays included)."""
+    rows = 50_000  # > 20 000 rows: the other columns have several pages
+    data, _ = W.config_c5(row_groups=(0, 1, 2), rows_per_rg=rows)
+    pf = pqgpu.ParquetFile(data)
+    assert pf.num_row_groups == 3
+    q12 = abi.QUIRK_Q1_PAGE_NILS | abi.QUIRK_Q2_DICT_ALIAS
+    for c in range(pf.num_columns):
+        jobs = [pf.host_job(rg, c)[0] for rg in range(3)]
+        for j in jobs:
+            ch = O.decode_chunk(j)
+            assert ch.status == 0
+            data_pages = [p for p in ch.pages if p.page_type != abi.PAGE_DICTIONARY]
+            has_dict = any(p.page_type == abi.PAGE_DICTIONARY for p in ch.pages)
+            has_nulls = ch.num_values < ch.num_slots
+            if has_dict or has_nulls:
+                assert len(data_pages) == 1, (pf.columns[c].path, len(data_pages))
+        spec = O.decode_column_store(jobs, 0)
+        quirky = O.decode_column_store(jobs, q12)
+        for rg in range(3):
+            _store_reads_equal(spec[rg], quirky[rg])
+
+
+def test_byte_array_store_q2_alias():
+    """pqo_decode_column_store on byte arrays: a 2-row-group x 2-page string
+    dictionary column shows Q2 from the second row group on (the store's
+    entries after page 1 differ from the spec decode), not in the first."""
+    rng = np.random.default_rng(5)
+    words = [b"w%02d" % i for i in range(6)]
+    keys = rng.integers(0, 6, size=ROWS)
+    lens = np.array([len(words[k]) for k in keys])
+    offs = np.zeros(ROWS + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    chars = np.frombuffer(b"".join(words[k] for k in keys), np.uint8).copy()
+    col = W.Column("s", W.BYTE_ARRAY, chars, offsets=offs, encoding=W.RLE_DICTIONARY, rows_per_page=ROWS // 4)
+    data = W.write_file([col], ROWS, row_groups=2)
+    pf = pqgpu.ParquetFile(data)
+    jobs = [pf.host_job(rg, 0)[0] for rg in range(2)]
+    spec = O.decode_column_store(jobs, 0)
+    q12 = O.decode_column_store(jobs, abi.QUIRK_Q1_PAGE_NILS | abi.QUIRK_Q2_DICT_ALIAS)
+    _store_equal(spec[0], q12[0])
+    (c0, o0), (c1, o1) = spec[1][1], q12[1][1]
+    assert len(o0) == len(o1) == ROWS // 2 + 1
+    assert not (np.array_equal(c0, c1) and np.array_equal(o0, o1))
+    # the spec store is the chunk's own decode
+    ch = O.decode_chunk(jobs[1])
+    assert np.array_equal(c0, ch.values) and np.array_equal(o0, ch.offsets)
