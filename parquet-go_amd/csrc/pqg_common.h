@@ -195,6 +195,73 @@ struct JobDev {
   int64_t run_cap, run_base;   // RunEnt arena region
   int64_t blk_cap, blk_base;   // block-index arena region
   int64_t run_used, blk_used;  // run-table / block-index entries the pages need (k_page_list)
+  // ---- values-stage work items of the job (k_part_plan): parts [item_base, item_base + n_items)
+  int64_t item_base;
+  int32_t n_items, pad2;
+};
+
+// ---------------------------------------------------------------------------
+// Big pages (parquet-go's own writer puts a whole column chunk in ONE data
+// page, chunk_writer.go:237-246, with each level / index stream one
+// bit-packed run, hybrid_encoder.go:59-73).  The values stages work on PARTS:
+// a page of at most kSplitMin values is one part; a bigger one is cut into
+// parts of about kPart values, each decoded by its own wave / workgroup.
+//   PLAIN (fixed width or byte arrays): values [p kPart, (p + 1) kPart)
+//   hybrid value streams (dictionary indices, RLE booleans): the blocks of the
+//     stream's block index whose first value lies in [p kPart, (p + 1) kPart)
+// Long runs inside the serial walks are handed to parallel kernels: level
+// runs of more than kLongLev values (k_level_long) and value-stream bit-packed
+// runs of more than kLongWalk values (k_walk_long).
+// ---------------------------------------------------------------------------
+constexpr int kSplitMin = 65536;
+constexpr int kPart = 4096;
+constexpr int kLongLev = 32768;
+constexpr int kLevPiece = 16384;
+constexpr int kLongWalk = 16384;
+// counters (ints after the counters base, zeroed by k_page_list)
+constexpr int kCtrItems = 48;     // values-stage parts of the batch
+constexpr int kCtrLongLev = 49;   // long level runs
+constexpr int kCtrLevPieces = 50; // pieces of the long level runs
+constexpr int kCtrLongWalk = 51;  // long bit-packed runs of value streams
+
+struct PartRec {
+  int32_t pidx;    // PageDev index
+  int32_t p, np;   // part p of np
+  uint32_t v0;     // first value (page-relative); the part ends at the next part's v0, or the page's count
+  int32_t b0;      // hybrid parts: first block (stream-relative); the part's blocks end at the next part's b0
+  int32_t vmode;   // the page's values stage (PageDev.vmode)
+  int64_t chars;   // byte arrays: chars of the part (k_str_count / k_char_scan)
+  int64_t cstart;  // byte arrays: chunk char offset of the part's first value (k_char_scan)
+  int64_t prel;    // byte arrays: page-relative char offset of the part's first value (k_char_scan)
+};
+
+// A level run of more than kLongLev values, expanded by k_level_long in
+// pieces of kLevPiece values.
+struct LongLev {
+  uint8_t* out;       // level bytes of the run's first value
+  const uint8_t* p;   // bit-packed: the run's payload (byte of its first value's bit 0); null for RLE
+  const uint8_t* end; // stream end (bytes at or past it read as zero: the short-read padding, Q5)
+  uint32_t count;     // values
+  uint32_t value;     // RLE value
+  int32_t w;          // bit width (1..8)
+  int32_t maxl;       // def levels: maxD (notNull counted into the page); rep levels: 0x100
+  int32_t pidx;       // PageDev index
+  int32_t pad;
+};
+struct LevPiece {
+  int32_t run;        // LongLev index
+  uint32_t v0, v1;    // values of the run
+};
+
+// A bit-packed run of a value stream longer than kLongWalk values: its block
+// descriptors (K values each) are written by k_walk_long.
+struct LongWalk {
+  int64_t blk;        // BlockDesc index (absolute) of the run's first block
+  uint32_t v0;        // first value of the run (stream-relative)
+  uint32_t take;      // values of the run that are used
+  uint32_t run;       // its run-table index (stream-relative)
+  uint32_t src;       // stream offset of its payload
+  int32_t w, K;       // bit width, values per block
 };
 
 // k_hybrid_walk block size: its LDS layout (pqg_levels.hip) and its launch
@@ -217,7 +284,8 @@ constexpr int kQueueSnapSerial = 10;
 // DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY lengths (k_str_delta) and values (k_str_dba)
 constexpr int kQueueStrDelta = 11;
 constexpr int kQueueStrDba = 12;
-constexpr int kQueueSlots = 13;  // queue regions zeroed per launch: 0-8, the stage flags (9), 10-12
+constexpr int kQueueLevLong = 13;  // pieces of the long level runs (k_level_long)
+constexpr int kQueueSlots = 14;  // queue regions zeroed per launch: 0-8, the stage flags (9), 10-13
 
 // Scan tiles of the speculative page-header search.
 constexpr int kScanTile = 16384;

@@ -290,9 +290,12 @@ __device__ __forceinline__ int64_t dict_page(PieceShared& ps, const gcu8 sp, con
   os.first = (uintptr_t)out;
   os.gaddr = os.first & ~(uintptr_t)15;
   os.carry = (uint32_t)((os.first - os.gaddr) >> 2);
+  if (nb_all <= 0) return bad;
   int kb = 0;
-  uint32_t rcur = 0;   // first run of block kb
-  int64_t pos = 0;     // stream offset of the payload window (before alignment)
+  // a part of a big page starts at any block: its first run and payload byte
+  const uint4 d0 = ldg16((uintptr_t)blks);
+  uint32_t rcur = d0.y;                 // first run of block kb
+  int64_t pos = (d0.w & 0xffffu) ? (int64_t)d0.z : 0;  // stream offset of the payload window (before alignment)
   while (kb < nb_all) {
     PQG_DT(ta);
     // ---- one round of loads: descriptors, run entries, payload window
@@ -383,19 +386,22 @@ __device__ __forceinline__ int64_t dict_page(PieceShared& ps, const gcu8 sp, con
 // Read phase of every 4-byte dictionary page in the list, and its VRec at the
 // page's list position (valuesDecoder.init type_dict.go:22-37: the bit-width
 // byte, > 32 is an error).
-__global__ void __launch_bounds__(256) k_dict_plan(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+// One VRec per work item (a page's part, k_part_plan): a part of a big page is
+// its blocks [b0, next part's b0) and values [v0, next part's v0).
+__global__ void __launch_bounds__(256) k_dict_plan(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total,
                                                    uint8_t* value_arena, const HStream* streams, const RunEnt* runs,
                                                    const BlockDesc* blks, VRec* recs) {
   if (total[kModePresentOff + 1] == 0) return;
-  const int nt = *total;
+  const int nt = total[kCtrItems];
   for (int t = blockIdx.x * 256 + threadIdx.x; t < nt; t += gridDim.x * 256) {
     VRec r;
     memset(&r, 0, sizeof(r));
     r.job = -1;
-    const int pidx = list[t];
+    const PartRec pr = parts[t];
+    const int pidx = pr.pidx;
     r.pidx = pidx;
     PageDev& P = pages[pidx];
-    if (P.read_status == kOK && (P.page_type == 0 || P.page_type == 3) && P.vmode == 1) {
+    if (pr.vmode == 1 && P.read_status == kOK && (P.page_type == 0 || P.page_type == 3) && P.vmode == 1) {
       const JobDev& J = jobs[P.job];
       if (J.status != kCAPACITY) {
         int re = kOK, dw = 0;
@@ -414,12 +420,16 @@ __global__ void __launch_bounds__(256) k_dict_plan(JobDev* jobs, PageDev* pages,
           r.w = dw;
           if (dw > 0) {
             const HStream& S = streams[P.hs_val];
+            const bool last = pr.p + 1 >= pr.np;
+            const int b1 = last ? S.n_blocks : parts[t + 1].b0;
             r.p = S.p;
             r.n = (int32_t)S.n;
             r.runs = runs + S.run_base;
-            r.blks = blks + S.blk_base;
-            r.n_blocks = S.n_blocks;
+            r.blks = blks + S.blk_base + pr.b0;
+            r.n_blocks = b1 - pr.b0;
             r.count = S.produced < r.nn ? S.produced : r.nn;
+            if (!last && (int32_t)parts[t + 1].v0 < r.count) r.count = (int32_t)parts[t + 1].v0;
+            r.out = value_arena + J.value_base + (P.value_offset + pr.v0) * 4;
             r.produced = S.produced;
             r.serr = (S.status != kOK && S.produced < r.nn) ? S.status : kOK;
           }
@@ -439,7 +449,7 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, kDWaves * 64), amd
   if (total[kModePresentOff + 1] == 0) return;  // no page of this stage
   if (threadIdx.x == 0) sh.dict_job = -1;
   PieceShared& ps = sh.w[wid];
-  const int nt = *total;
+  const int nt = total[kCtrItems];  // work items: pages' parts (k_part_plan)
   DProf pf;
   for (;;) {
     PQG_DT(t0);
@@ -524,7 +534,7 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, kDWaves * 64), amd
       if (bad < r.nn && (r.serr == kOK || bad < r.produced)) de = kDICT_INDEX;
       else de = r.serr;
     }
-    if (lane == 0 && de != kOK) pages[r.pidx].decode_status = de;
+    if (lane == 0 && de != kOK) atomicMin(&pages[r.pidx].decode_status, de);  // parts of a page: kDICT_INDEX wins
     PQG_DT(t3);
     pf.add(6, 1);
     pf.add(9, t3 - t2);

@@ -146,10 +146,12 @@ __device__ __forceinline__ void block_values_1(const ExpandShared& sh, int b, co
 // loads, so that (vmcnt retires in issue order) the wait for the gathers
 // never includes those loads, the wait for those loads never includes this
 // group's stores, and the gather and payload latencies overlap.
+// Blocks [blo, bhi) of the stream (a part of a big page, pqg_common.h; the
+// whole stream: 0, S.n_blocks), values below `count`.
 template <class Sink>
 __device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __restrict__ runs_,
                                               const BlockDesc* __restrict__ blks_, int64_t count, ExpandShared& sh,
-                                              Sink& sink) {
+                                              Sink& sink, int blo = 0, int bhi = -1) {
   const int lane = lane_id();
   const int w = S.w;
   const uint32_t mask = w == 32 ? 0xffffffffu : ((1u << w) - 1);
@@ -161,8 +163,8 @@ __device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __
   const int64_t n = S.n;
   const PQG_G RunEnt* runs = gconst(runs_) + S.run_base;
   const PQG_G BlockDesc* blks = gconst(blks_) + S.blk_base;
-  const int nb_all = S.n_blocks;
-  for (int b0 = 0; b0 < nb_all; b0 += 64) {
+  const int nb_all = bhi < 0 || bhi > S.n_blocks ? S.n_blocks : bhi;
+  for (int b0 = blo; b0 < nb_all; b0 += 64) {
     const int nb = nb_all - b0 < 64 ? nb_all - b0 : 64;
     __builtin_amdgcn_wave_barrier();
     if (lane < nb) {
@@ -179,7 +181,7 @@ __device__ __forceinline__ void hybrid_expand(const HStream& S, const RunEnt* __
     if (nk == 0) break;
     // the last block here ends at the next batch's first block, or at count
     uint32_t tail_end = end_all;
-    if (nk == nb && b0 + nb < nb_all) {
+    if (nk == nb && b0 + nb < S.n_blocks) {
       const uint32_t nv0 = blks[b0 + nb].v0;
       tail_end = nv0 < end_all ? nv0 : end_all;
     }

@@ -132,9 +132,11 @@ struct LaneRing {
 // Lanes [0, total) walk the rep streams, [total, 2 total) the def streams,
 // [2 total, 3 total) the value streams, so a wave's lanes do alike work.
 __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pages, const int* list, const int* total,
-                                                              HStream* streams, RunEnt* runs, BlockDesc* blks) {
+                                                              HStream* streams, RunEnt* runs, BlockDesc* blks,
+                                                              LongWalk* longs, int long_cap) {
   __shared__ uint32_t buf[32 * kWalkThreads];  // two 64-byte chunks per lane
   const int nt = *total;
+  int* const n_long = const_cast<int*>(total) + kCtrLongWalk;
   // level streams are decoded in place by k_page_levels: only the value streams
   // (dictionary indices, RLE booleans) are walked
   for (int g = blockIdx.x * kWalkThreads + threadIdx.x; g < nt; g += gridDim.x * kWalkThreads) {
@@ -224,8 +226,37 @@ __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pag
       }
       if (take > 0) {
         stg8((uintptr_t)(R + 2 * nr), st, src);
-        // the run joins the open block, and every block it reaches into
         const uint32_t rend = produced + take;
+        if ((st & kRunBP) && take > (uint32_t)kLongWalk) {
+          // a long bit-packed run (parquet-go's writer: the whole stream): its
+          // blocks of K values each are written by k_walk_long in parallel
+          const uint32_t K = min((uint32_t)kHBlock, ((8u * kHBlockBytes - 14u) / w) & ~7u);
+          const uint32_t R = (take + K - 1) / K;
+          const int li = atomicAdd(n_long, 1);
+          if (li < long_cap) {
+            close_block();
+            LongWalk L;
+            L.blk = S.blk_base + nb;
+            L.v0 = produced;
+            L.take = take;
+            L.run = nr;
+            L.src = src;
+            L.w = (int32_t)w;
+            L.K = (int32_t)K;
+            longs[li] = L;
+            nb += R;
+            bv0 = rend;  // the next run opens a new block
+            br0 = nr + 1;
+            bn = 0;
+            blo = ~0ull;
+            bhi = 0;
+            produced = rend;
+            nr++;
+            if (status) break;
+            continue;
+          }
+        }
+        // the run joins the open block, and every block it reaches into
         for (uint32_t v = produced; v < rend;) {
           if (bn == kHBlockRuns || v >= bv0 + kHBlock) {
             close_block();
@@ -270,6 +301,94 @@ __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pag
     S.produced = (int32_t)produced;
     S.status = status;
     S.n_blocks = (int32_t)nb;
+  }
+}
+
+// The block descriptors of the long bit-packed runs k_hybrid_walk handed
+// over: block j of a run holds values [v0 + j K, v0 + min((j + 1) K, take)),
+// one run, its payload bytes from the bit of its first value.  Every thread of
+// the grid takes blocks of every run.
+__global__ void __launch_bounds__(256) k_walk_long(const int* ctr, const LongWalk* longs, int long_cap,
+                                                   BlockDesc* blks) {
+  const int n = min(ctr[kCtrLongWalk], long_cap);
+  const uint32_t tid = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
+  for (int r = 0; r < n; r++) {
+    const LongWalk L = longs[r];
+    const uint32_t R = (L.take + (uint32_t)L.K - 1) / (uint32_t)L.K;
+    for (uint32_t j = tid; j < R; j += stride) {
+      const uint32_t a = j * (uint32_t)L.K;
+      const uint32_t cnt = min((uint32_t)L.K, L.take - a);
+      const uint64_t bit0 = (uint64_t)L.src * 8 + (uint64_t)a * (uint32_t)L.w;
+      const uint64_t lo = bit0 >> 3, hi = (bit0 + (uint64_t)cnt * (uint32_t)L.w + 7) >> 3;
+      stg16((uintptr_t)(blks + L.blk + j),
+            make_uint4(L.v0 + a, L.run, (uint32_t)lo, (uint32_t)(hi - lo) | (1u << 16)));
+    }
+  }
+}
+
+// Long level runs (more than kLongLev values, recorded by k_page_levels):
+// one wave per piece of kLevPiece values, 16 values per lane per step; the
+// level bytes leave as aligned 16-byte granules (the piece's ragged ends
+// byte by byte), notNull is added to the page.
+__global__ void __launch_bounds__(64) k_level_long(PageDev* pages, const int* ctr, const LongLev* longs, int long_cap,
+                                                   const LevPiece* pieces, int piece_cap, int* queue) {
+  const int lane = lane_id();
+  const int np = min(ctr[kCtrLevPieces], piece_cap);
+  for (;;) {
+    const int t = queue_next(queue);
+    if (t >= np) return;
+    const LevPiece pc = pieces[t];
+    if (pc.run < 0 || pc.run >= long_cap) continue;
+    const LongLev L = longs[pc.run];
+    if (pages[L.pidx].decode_status != kOK) continue;  // a failing page: its levels are not used
+    const uintptr_t ob = (uintptr_t)L.out;
+    const uint32_t mask = (1u << L.w) - 1;
+    const int64_t navail = L.p ? (int64_t)(L.end - L.p) : 0;
+    uint32_t nn = 0;
+    const uintptr_t a0 = (ob + pc.v0) & ~(uintptr_t)15;
+    for (uintptr_t a = a0 + 16 * (uintptr_t)lane; a < ob + pc.v1; a += 1024) {
+      const int64_t i0 = (int64_t)(a - ob);  // value of the granule's byte 0 (may be < v0)
+      uint32_t v[16];
+      if (L.p) {
+        const int64_t ib = i0 < 0 ? 0 : i0;
+        const int64_t bit = ib * L.w;
+        const gcu8 p = gconst(L.p);
+        const uint64_t x0 = load_u64_masked(p, navail, bit >> 3, navail);
+        const uint64_t x1 = load_u64_masked(p, navail, (bit >> 3) + 8, navail);
+        const uint32_t sh = (uint32_t)(bit & 7);
+        const int64_t shift0 = (i0 < 0 ? -i0 : 0) * L.w;  // granule values before value 0 (never stored)
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+          const int64_t b = (int64_t)sh + (int64_t)k * L.w - shift0;
+          uint32_t x = 0;
+          if (b >= 0) {
+            x = b < 64 ? (uint32_t)(x0 >> b) | (b > 56 ? (uint32_t)(x1 << (64 - b)) : 0u) : (uint32_t)(x1 >> (b - 64));
+          }
+          v[k] = x & mask;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = L.value;
+      }
+      uint32_t wv[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) wv[k] = v[4 * k] | v[4 * k + 1] << 8 | v[4 * k + 2] << 16 | v[4 * k + 3] << 24;
+      if (i0 >= (int64_t)pc.v0 && i0 + 16 <= (int64_t)pc.v1) {
+        stg16(a, make_uint4(wv[0], wv[1], wv[2], wv[3]));
+#pragma unroll
+        for (int k = 0; k < 16; k++) nn += v[k] == (uint32_t)L.maxl;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+          if (i0 + k >= (int64_t)pc.v0 && i0 + k < (int64_t)pc.v1) {
+            *(PQG_G uint8_t*)(a + k) = (uint8_t)v[k];
+            nn += v[k] == (uint32_t)L.maxl;
+          }
+        }
+      }
+    }
+    const int64_t tot = wave_sum((int64_t)nn);
+    if (lane == 0 && L.maxl <= 255 && tot) atomicAdd(&pages[L.pidx].not_null, (int32_t)tot);
   }
 }
 
@@ -406,6 +525,11 @@ struct LevelDecoder {
   gu8 out;         // count bytes
   uint32_t maxl;
   LevShared* sh;
+  // long runs (> kLongLev values) go to k_level_long (null: expanded here)
+  LongLev* longs;
+  LevPiece* pieces;
+  int* ctr;
+  int long_cap, piece_cap, pidx;
   uint32_t wbase = 0;  // stream offset of win[0] (16-aligned in memory, may precede the stream)
   bool have = false;
   uint32_t nn = 0;     // per lane: values == maxl
@@ -784,6 +908,45 @@ struct LevelDecoder {
     return long_run_fields(bp, cnt, pay, nx, produced, pos);
   }
 
+  // Record the run [produced, produced + take) for k_level_long (pieces of
+  // kLevPiece values); false (nothing recorded) when the tables are full.
+  __device__ bool defer_long(bool bp, uint32_t take, uint32_t pay, uint32_t produced) {
+    const int lane = lane_id();
+    const uint32_t P = (take + kLevPiece - 1) / kLevPiece;
+    int li = 0, pb = 0;
+    if (lane == 0) {
+      li = atomicAdd(ctr + kCtrLongLev, 1);
+      pb = li < long_cap ? atomicAdd(ctr + kCtrLevPieces, (int)P) : 0;
+    }
+    li = __builtin_amdgcn_readfirstlane(li);
+    pb = __builtin_amdgcn_readfirstlane(pb);
+    if (li >= long_cap) return false;
+    const bool ok = (int64_t)pb + P <= (int64_t)piece_cap;
+    if (lane == 0) {
+      LongLev L;
+      L.out = (uint8_t*)(out + produced);
+      L.p = bp ? (const uint8_t*)(p + pay) : nullptr;
+      L.end = (const uint8_t*)(p + n);
+      L.count = take;
+      L.value = bp ? 0u : pay;
+      L.w = w;
+      L.maxl = (int32_t)maxl;
+      L.pidx = pidx;
+      L.pad = 0;
+      longs[li] = L;
+    }
+    // the reserved pieces (those inside the table): the run's, or empty when
+    // the table cannot hold them all (the run is then expanded here)
+    for (uint32_t j = (uint32_t)lane; j < P && (int64_t)pb + j < (int64_t)piece_cap; j += 64) {
+      LevPiece pc;
+      pc.run = ok ? li : -1;
+      pc.v0 = j * kLevPiece;
+      pc.v1 = min(take, (j + 1) * (uint32_t)kLevPiece);
+      pieces[pb + j] = pc;
+    }
+    return ok;
+  }
+
   __device__ int long_run_fields(bool bp, uint32_t cnt, uint32_t pay, uint32_t nx, uint32_t& produced, uint32_t& pos) {
     const int lane = lane_id();
     const uint32_t left = count - produced;
@@ -798,6 +961,11 @@ struct LevelDecoder {
       }
     }
     if (status != kOK) return status;  // levels: the values of a failing stream do not matter
+    if (take > (uint32_t)kLongLev && longs && defer_long(bp, take, pay, produced)) {
+      produced += take;
+      pos = nx;
+      return kOK;
+    }
     uint32_t done = 0;
     while (done < take) {
       const uint32_t pre = (uint32_t)(((uintptr_t)out + produced) & 15);
@@ -837,9 +1005,16 @@ struct LevelDecoder {
   }
 };
 
+struct LongTables {
+  LongLev* longs;
+  LevPiece* pieces;
+  int* ctr;
+  int long_cap, piece_cap;
+};
+
 __device__ __forceinline__ int level_stream(gcu8 p, int64_t n, int w, uint32_t count, gu8 out, uint32_t maxl,
-                                            LevShared& sh, uint32_t* nn) {
-  LevelDecoder dec{p, (uint32_t)n, w, count, out, maxl, &sh};
+                                            LevShared& sh, uint32_t* nn, const LongTables& lt, int pidx) {
+  LevelDecoder dec{p, (uint32_t)n, w, count, out, maxl, &sh, lt.longs, lt.pieces, lt.ctr, lt.long_cap, lt.piece_cap, pidx};
   const int e = dec.run();
 #ifdef PQG_PROFILE
   for (int k = 0; k < 8; k++) PQG_ACC(k, 0, dec.pacc[k]);
@@ -853,9 +1028,11 @@ __device__ __forceinline__ int level_stream(gcu8 p, int64_t n, int w, uint32_t c
 // registered for the walker.
 __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total,
                                                     int* queue, uint8_t* scratch, HStream* streams,
-                                                    uint8_t* def_arena, uint8_t* rep_arena) {
+                                                    uint8_t* def_arena, uint8_t* rep_arena, LongLev* longs,
+                                                    int long_cap, LevPiece* pieces, int piece_cap) {
   __shared__ __attribute__((aligned(16))) LevShared sh;
   const int lane = lane_id();
+  const LongTables lt{longs, pieces, const_cast<int*>(total), long_cap, piece_cap};
   for (;;) {
     const int t = queue_next(queue);
     if (t >= *total) return;
@@ -961,7 +1138,7 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
         else {
           uint32_t unused;
           de = level_stream(rep, rep_n, bits_len((uint32_t)job.max_rep), (uint32_t)n,
-                            gmut(rep_arena) + job.slot_base + pg.slot_offset, 0x100u, sh, &unused);
+                            gmut(rep_arena) + job.slot_base + pg.slot_offset, 0x100u, sh, &unused, lt, pidx);
         }
       }
       if (de == kOK) {
@@ -970,7 +1147,8 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
           else {
             uint32_t c;
             de = level_stream(def, def_n, bits_len((uint32_t)job.max_def), (uint32_t)n,
-                              gmut(def_arena) + job.slot_base + pg.slot_offset, (uint32_t)job.max_def, sh, &c);
+                              gmut(def_arena) + job.slot_base + pg.slot_offset, (uint32_t)job.max_def, sh, &c, lt,
+                              pidx);
             nn = c;
           }
         } else {
@@ -1058,6 +1236,150 @@ __global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, 
         }
       }
     }
+  }
+}
+
+}  // namespace pqg
+
+namespace pqg {
+
+// ---- values-stage parts -----------------------------------------------------
+// Per job (one 1024-thread block, after k_nn_scan): every set-up data page
+// gets one PartRec, a page of more than kSplitMin values (parquet-go's writer:
+// the whole chunk) several (see pqg_common.h); the job's parts are contiguous,
+// in page order, from a slot range taken with one atomic.
+__device__ __forceinline__ int64_t part_count(const PageDev& pg, const HStream* streams, bool* hyb) {
+  *hyb = false;
+  if ((pg.page_type != 0 && pg.page_type != 3) || pg.vmode < 0) return -1;  // no part
+  if (pg.read_status != kOK || pg.decode_status != kOK || pg.vmode == 3) return 0;  // one part
+  const int enc = pg.encoding;
+  if (pg.vmode == 2 && enc != 0 && enc != 8) return 0;  // DELTA_(LENGTH_)BYTE_ARRAY: one part
+  const int64_t nn = pg.not_null;
+  if (enc == 0) return nn;                                // PLAIN: value ranges
+  if ((enc == 8 || enc == 3) && pg.hs_val >= 0) {         // hybrid value stream: block ranges
+    const HStream& S = streams[pg.hs_val];
+    *hyb = true;
+    return nn < S.produced ? nn : S.produced;
+  }
+  return 0;
+}
+
+__global__ void __launch_bounds__(1024) k_part_plan(JobDev* jobs, const PageDev* pages, const HStream* streams,
+                                                    const BlockDesc* blks, int* ctr, PartRec* parts, int64_t cap) {
+  __shared__ int64_t part[17];
+  __shared__ int64_t s_base;
+  __shared__ int s_big[1024];  // pages of this round that are split
+  __shared__ int s_nbig;
+  JobDev& job = jobs[blockIdx.x];
+  int np = job.num_pages < job.page_cap ? job.num_pages : job.page_cap;
+  if (job.status == kCAPACITY) np = 0;
+  const PageDev* pp = pages + job.page_base;
+  auto nparts = [&](int i, int64_t* count, bool* hyb) -> int64_t {
+    const int64_t c = part_count(pp[i], streams, hyb);
+    *count = c;
+    if (c < 0) return 0;
+    return c > kSplitMin ? (c + kPart - 1) / kPart : 1;
+  };
+  // pass 1: parts per page, the job's slot range
+  int64_t tot_all = 0;
+  for (int b = 0; b < np; b += 1024) {
+    const int i = b + (int)threadIdx.x;
+    int64_t c;
+    bool h;
+    const int64_t k = i < np ? nparts(i, &c, &h) : 0;
+    int64_t tot;
+    block_excl_scan<1024>(k, &tot, part);
+    tot_all += tot;
+  }
+  if (threadIdx.x == 0) {
+    int64_t base = atomicAdd(ctr + kCtrItems, (int)tot_all);
+    if (base + tot_all > cap) {
+      job.status = kCAPACITY;
+      tot_all = 0;
+    }
+    job.item_base = base;
+    job.n_items = (int32_t)tot_all;
+    s_base = base;
+  }
+  __syncthreads();
+  if (job.status == kCAPACITY) return;
+  const int64_t base = s_base;
+  // pass 2: single-part pages; the split ones are listed for pass 3
+  int64_t carry = 0;
+  for (int b = 0; b < np; b += 1024) {
+    const int i = b + (int)threadIdx.x;
+    int64_t c = 0;
+    bool h = false;
+    const int64_t k = i < np ? nparts(i, &c, &h) : 0;
+    int64_t tot;
+    const int64_t ex = carry + block_excl_scan<1024>(k, &tot, part);
+    carry += tot;
+    if (threadIdx.x == 0) s_nbig = 0;
+    __syncthreads();
+    if (k == 1) {
+      PartRec r;
+      r.pidx = (int32_t)(job.page_base + i);
+      r.p = 0;
+      r.np = 1;
+      r.v0 = 0;
+      r.b0 = 0;
+      r.vmode = pp[i].vmode;
+      r.chars = r.cstart = r.prel = 0;
+      parts[base + ex] = r;
+    } else if (k > 1) {
+      s_big[atomicAdd(&s_nbig, 1)] = i;
+    }
+    __syncthreads();
+    // pass 3: the split pages of this round, every thread on each
+    const int nbig = s_nbig;
+    for (int q = 0; q < nbig; q++) {
+      const int pi = s_big[q];
+      int64_t cnt;
+      bool hyb;
+      const int64_t P = nparts(pi, &cnt, &hyb);
+      // the page's first slot: its exclusive offset (recomputed: pages before it in this round)
+      __shared__ int64_t s_off;
+      if (i == pi) s_off = ex;
+      __syncthreads();
+      const int64_t off = s_off;
+      __syncthreads();
+      const PageDev& pg = pp[pi];
+      PartRec r;
+      r.pidx = (int32_t)(job.page_base + pi);
+      r.np = (int32_t)P;
+      r.vmode = pg.vmode;
+      r.chars = r.cstart = r.prel = 0;
+      if (!hyb) {
+        for (int64_t p = threadIdx.x; p < P; p += 1024) {
+          r.p = (int32_t)p;
+          r.v0 = (uint32_t)(p * kPart);
+          r.b0 = 0;
+          parts[base + off + p] = r;
+        }
+      } else {
+        // part q starts at the first block whose first value is >= q kPart
+        // (blocks hold <= kHBlock <= kPart values, so every part but an
+        // empty tail one has a block start)
+        const HStream& S = streams[pg.hs_val];
+        const BlockDesc* B = blks + S.blk_base;
+        const int nb = S.n_blocks;
+        auto f = [&](int bi) -> int64_t {
+          if (bi < 0) return -1;
+          if (bi >= nb || (int64_t)B[bi].v0 >= cnt) return P;
+          return (int64_t)B[bi].v0 / kPart;
+        };
+        for (int bi = threadIdx.x; bi <= nb; bi += 1024) {
+          const int64_t f1 = f(bi), f0 = f(bi - 1);
+          for (int64_t p = f0 + 1; p <= f1 && p < P; p++) {
+            r.p = (int32_t)p;
+            r.v0 = p == 0 ? 0u : (bi < nb && (int64_t)B[bi].v0 < cnt ? B[bi].v0 : (uint32_t)cnt);
+            r.b0 = bi;
+            parts[base + off + p] = r;
+          }
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 

@@ -53,28 +53,35 @@ __global__ void k_snap_link(const JobDev* jobs, PageDev* pages, const int* list,
 __global__ void k_snap_decode(const JobDev* jobs, PageDev* pages, const SnapSub* subs, const int* sub_total,
                               int sub_cap, int* queue, uint8_t* scratch);
 __global__ void k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
-                              uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena);
+                              uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena,
+                              LongLev* longs, int long_cap, LevPiece* pieces, int piece_cap);
+__global__ void k_level_long(PageDev* pages, const int* ctr, const LongLev* longs, int long_cap,
+                             const LevPiece* pieces, int piece_cap, int* queue);
 __global__ void k_hybrid_walk(const PageDev* pages, const int* list, const int* total, HStream* streams,
-                              RunEnt* runs, BlockDesc* blks);
+                              RunEnt* runs, BlockDesc* blks, LongWalk* longs, int long_cap);
+__global__ void k_walk_long(const int* ctr, const LongWalk* longs, int long_cap, BlockDesc* blks);
 __global__ void k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch);
+__global__ void k_part_plan(JobDev* jobs, const PageDev* pages, const HStream* streams, const BlockDesc* blks,
+                            int* ctr, PartRec* parts, int64_t cap);
 template <int Mode>
-__global__ void k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+__global__ void k_values(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total, int* queue,
                          uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks);
-__global__ void k_dict_plan(JobDev* jobs, PageDev* pages, const int* list, const int* total, uint8_t* value_arena,
-                            const HStream* streams, const RunEnt* runs, const BlockDesc* blks, VRec* recs);
+__global__ void k_dict_plan(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total,
+                            uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks,
+                            VRec* recs);
 __global__ void k_dict4(PageDev* pages, const int* total, int* queue, const VRec* recs);
 __global__ void k_finalize(JobDev* jobs, int n_jobs, PageDev* pages);
 __global__ void k_str_dict(JobDev* jobs, PageDev* pages, int64_t* doffs_arena);
-__global__ void k_str_count(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+__global__ void k_str_count(JobDev* jobs, PageDev* pages, PartRec* parts, const int* total, int* queue,
                             int64_t* offs_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks);
 __global__ void k_str_plain(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                             int64_t* offs_arena);
-__global__ void k_char_scan(JobDev* jobs, PageDev* pages, int64_t* offs_arena);
+__global__ void k_char_scan(JobDev* jobs, PageDev* pages, PartRec* parts, int64_t* offs_arena);
 __global__ void k_str_delta(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                             int64_t* offs_arena);
 __global__ void k_str_dba(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                           uint8_t* value_arena, int64_t* offs_arena);
-__global__ void k_str_copy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+__global__ void k_str_copy(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total, int* queue,
                            uint8_t* value_arena, int64_t* offs_arena);
 }  // namespace pqg
 
@@ -176,6 +183,8 @@ struct pqg_ctx {
   DevBuf blk_src, blk_dst, blk_meta, blk_subs, blk_segpage, blk_F;  // pqg_block_decompress
   DevBuf sn_subs, sn_segpage, sn_F;   // K2 split: sub-block table, segment -> page, segment exits
   int64_t sn_sub_cap = 0, sn_seg_cap = 0;
+  DevBuf parts, lev_long, lev_pieces, walk_long;  // big pages: values-stage parts, long level / value-stream runs
+  int64_t parts_cap = 0, lev_long_cap = 0, lev_piece_cap = 0, walk_long_cap = 0;
   int64_t total_tiles = 0;
   JobDev* h_jobs = nullptr;  // pinned
   int h_jobs_cap = 0;
@@ -272,7 +281,8 @@ void pqg_ctx_destroy(pqg_ctx* c) {
                     &c->scratch, &c->streams, &c->runs, &c->blks, &c->cand_list, &c->vlists, &c->tile_count, &c->tile_okc, &c->tile_off, &c->tile_okoff, &c->cand_pos, &c->cands, &c->succ, &c->idx2slot,
                     &c->ok2slot, &c->order, &c->asm_seg, &c->offs_arena, &c->doffs_arena, &c->page_stage,
                     &c->blk_src, &c->blk_dst, &c->blk_meta, &c->tile_job, &c->sn_subs, &c->sn_segpage, &c->sn_F,
-                    &c->blk_subs, &c->blk_segpage, &c->blk_F, &c->vrecs})
+                    &c->blk_subs, &c->blk_segpage, &c->blk_F, &c->vrecs, &c->parts, &c->lev_long, &c->lev_pieces,
+                    &c->walk_long})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
   hipStreamDestroy(c->stream);
@@ -391,6 +401,17 @@ static int plan_batch(pqg_ctx* c) {
     c->h_jobs[i] = d;
   }
   c->list_cap = page_total;
+  // big pages (pqg_common.h): a page of nn values has <= nn / kPart + 1 parts;
+  // a long level run (rep and def streams) has > kLongLev values, a long
+  // value-stream run > kLongWalk
+  c->parts_cap = page_total + slot_total / kPart + n + 64;
+  c->lev_long_cap = 2 * slot_total / kLongLev + 64;
+  c->lev_piece_cap = 2 * slot_total / kLevPiece + 2 * c->lev_long_cap + 64;
+  c->walk_long_cap = slot_total / kLongWalk + 64;
+  if (c->parts.grow(sizeof(PartRec) * (size_t)c->parts_cap) || c->lev_long.grow(sizeof(LongLev) * (size_t)c->lev_long_cap) ||
+      c->lev_pieces.grow(sizeof(LevPiece) * (size_t)c->lev_piece_cap) ||
+      c->walk_long.grow(sizeof(LongWalk) * (size_t)c->walk_long_cap))
+    return PQG_ERR_HIP;
   // K2 split tables: a page of u bytes has ceil(u / 64 KiB) sub-blocks (>= 1)
   // and a block of b bytes ceil(b / 4 KiB) segments
   c->sn_sub_cap = scratch_total / kSnapSub + page_total + 64;
@@ -415,7 +436,7 @@ static int plan_batch(pqg_ctx* c) {
       c->streams.grow(sizeof(HStream) * 3 * (size_t)page_total + 64) ||
       // slack past the last entry: k_dict4 stages run / descriptor granules past a stream's end
       c->runs.grow(sizeof(RunEnt) * (size_t)run_total + 8192) || c->blks.grow(sizeof(BlockDesc) * (size_t)blk_total + 8192) ||
-      c->vrecs.grow(sizeof(VRec) * (size_t)std::max<int64_t>(page_total, 1)) ||
+      c->vrecs.grow(sizeof(VRec) * (size_t)std::max<int64_t>(c->parts_cap, 1)) ||
       c->offs_arena.grow(sizeof(int64_t) * (size_t)offs_total + 64) ||
       c->doffs_arena.grow(sizeof(int64_t) * (size_t)doffs_total + 64))
     return PQG_ERR_HIP;
@@ -507,32 +528,45 @@ static int launch_pipeline(pqg_ctx* c) {
   HStream* streams = (HStream*)c->streams.p;
   RunEnt* runs = (RunEnt*)c->runs.p;
   BlockDesc* blks = (BlockDesc*)c->blks.p;
-  // setup + def/rep levels, one wave per data page (value streams registered for the walk)
+  // setup + def/rep levels, one wave per data page (value streams registered
+  // for the walk); long level runs then expand in pieces over the whole chip
+  LongLev* llong = (LongLev*)c->lev_long.p;
+  LevPiece* lpieces = (LevPiece*)c->lev_pieces.p;
+  const int llc = (int)std::min<int64_t>(c->lev_long_cap, INT32_MAX), lpc = (int)std::min<int64_t>(c->lev_piece_cap, INT32_MAX);
   hipLaunchKernelGGL(k_page_levels, dim3(qgrid(c->num_cus * 24)), dim3(64), 0, s, jobs, pages, list, ctr, Q(1), scratch,
-                     streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p);
+                     streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p, llong, llc, lpieces, lpc);
+  hipLaunchKernelGGL(k_level_long, dim3(qgrid(c->num_cus * 8)), dim3(64), 0, s, pages, ctr, llong, llc, lpieces, lpc,
+                     Q(kQueueLevLong));
   if (c->timed) hipEventRecord(c->ev[4], s);
   const unsigned walk_blocks = (unsigned)std::max<int64_t>(
       1, std::min<int64_t>((c->list_cap + kWalkLanes - 1) / kWalkLanes, c->num_cus * (2048 / kWalkLanes)));
-  hipLaunchKernelGGL(k_hybrid_walk, dim3(walk_blocks), dim3(kWalkLanes), 0, s, pages, list, ctr, streams, runs, blks);
+  LongWalk* wlong = (LongWalk*)c->walk_long.p;
+  const int wlc = (int)std::min<int64_t>(c->walk_long_cap, INT32_MAX);
+  hipLaunchKernelGGL(k_hybrid_walk, dim3(walk_blocks), dim3(kWalkLanes), 0, s, pages, list, ctr, streams, runs, blks,
+                     wlong, wlc);
+  hipLaunchKernelGGL(k_walk_long, dim3(c->num_cus * 2), dim3(256), 0, s, ctr, wlong, wlc, blks);
   if (c->timed) hipEventRecord(c->ev[5], s);
   if (c->timed) hipEventRecord(c->ev[6], s);
   hipLaunchKernelGGL(k_nn_scan, dim3(n), dim3(1024), 0, s, jobs, pages, scratch);
+  PartRec* parts = (PartRec*)c->parts.p;
+  hipLaunchKernelGGL(k_part_plan, dim3(n), dim3(1024), 0, s, jobs, pages, streams, blks, ctr, parts, c->parts_cap);
   if (c->timed) hipEventRecord(c->ev[7], s);
-  // every values kernel takes the whole page list and keeps the pages whose
-  // vmode (set by k_page_levels) is its own
+  // every values kernel takes the work items (the pages' parts) and keeps the
+  // ones whose vmode (set by k_page_levels) is its own
+  const int64_t items_cap = c->parts_cap;
   if (c->dict4) {  // 4-byte dictionary pages: pieces staged in LDS, small dictionaries in LDS (pqg_dict.hip)
     VRec* recs = (VRec*)c->vrecs.p;
-    hipLaunchKernelGGL(k_dict_plan, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((c->list_cap + 255) / 256, c->num_cus * 4))),
-                       dim3(256), 0, s, jobs, pages, list, ctr, (uint8_t*)c->value_arena.p, streams, runs, blks, recs);
+    hipLaunchKernelGGL(k_dict_plan, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((items_cap + 255) / 256, c->num_cus * 4))),
+                       dim3(256), 0, s, jobs, pages, parts, ctr, (uint8_t*)c->value_arena.p, streams, runs, blks, recs);
     hipLaunchKernelGGL(k_dict4, dim3(qgrid(c->num_cus * c->dict4_per_cu)), dim3(c->dict4_threads), 0, s, pages, ctr, Q(3),
                        recs);
   } else
-    hipLaunchKernelGGL(k_values<1>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(3),
+    hipLaunchKernelGGL(k_values<1>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, parts, ctr, Q(3),
                        (uint8_t*)c->value_arena.p, streams, runs, blks);
   if (c->any_fixed_other) {
-    hipLaunchKernelGGL(k_values<0>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(2),
+    hipLaunchKernelGGL(k_values<0>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, parts, ctr, Q(2),
                        (uint8_t*)c->value_arena.p, streams, runs, blks);
-    hipLaunchKernelGGL(k_values<3>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(8),
+    hipLaunchKernelGGL(k_values<3>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, parts, ctr, Q(8),
                        (uint8_t*)c->value_arena.p, streams, runs, blks);
   }
   if (c->timed) hipEventRecord(c->ev[8], s);
@@ -540,12 +574,12 @@ static int launch_pipeline(pqg_ctx* c) {
     int64_t* offs = (int64_t*)c->offs_arena.p;
     hipLaunchKernelGGL(k_str_dict, dim3(n), dim3(512), 0, s, jobs, pages, (int64_t*)c->doffs_arena.p);
     hipLaunchKernelGGL(k_str_plain, dim3(qgrid(c->num_cus * 4)), dim3(512), 0, s, jobs, pages, list, ctr, Q(5), offs);
-    hipLaunchKernelGGL(k_str_count, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, ctr, Q(4), offs, streams, runs,
-                       blks);
+    hipLaunchKernelGGL(k_str_count, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, parts, ctr, Q(4), offs, streams,
+                       runs, blks);
     hipLaunchKernelGGL(k_str_delta, dim3(qgrid(c->num_cus * 8)), dim3(64), 0, s, jobs, pages, list, ctr,
                        Q(kQueueStrDelta), offs);
-    hipLaunchKernelGGL(k_char_scan, dim3(n), dim3(256), 0, s, jobs, pages, offs);
-    hipLaunchKernelGGL(k_str_copy, dim3(qgrid(c->num_cus * 4)), dim3(512), 0, s, jobs, pages, list, ctr, Q(6),
+    hipLaunchKernelGGL(k_char_scan, dim3(n), dim3(256), 0, s, jobs, pages, parts, offs);
+    hipLaunchKernelGGL(k_str_copy, dim3(qgrid(c->num_cus * 4)), dim3(512), 0, s, jobs, pages, parts, ctr, Q(6),
                        (uint8_t*)c->value_arena.p, offs);
     hipLaunchKernelGGL(k_str_dba, dim3(qgrid(c->num_cus * 6)), dim3(64), 0, s, jobs, pages, list, ctr,
                        Q(kQueueStrDba), (uint8_t*)c->value_arena.p, offs);

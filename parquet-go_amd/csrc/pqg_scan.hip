@@ -762,6 +762,7 @@ __global__ void __launch_bounds__(1024) k_page_list(JobDev* jobs, PageDev* pages
       const int all = off + pages_of(j);
       *total = all < list_cap ? all : list_cap;
       for (int q = 0; q < 16; q++) queues[q] = 0;  // ctr[8..23]
+      for (int q = kCtrItems; q <= kCtrLongWalk; q++) queues[q - 8] = 0;  // the big-page counters
     }
   }
   __syncthreads();

@@ -382,15 +382,21 @@ __device__ __forceinline__ void copy_bytes(gu8 dst, gcu8 src, int64_t len) {
 }
 
 // ---- K7b ---------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_str_count(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+// Work items are the pages' parts (k_part_plan): a big dictionary page is
+// counted by many waves, each over its blocks; the part's chars go to its
+// PartRec (k_char_scan scans them).
+__global__ void __launch_bounds__(64) k_str_count(JobDev* jobs, PageDev* pages, PartRec* parts, const int* total,
                                                   int* queue, int64_t* offs_arena, const HStream* streams,
                                                   const RunEnt* runs, const BlockDesc* blks) {
   __shared__ __attribute__((aligned(16))) ExpandShared sh;
   const int lane = lane_id();
+  const int n_items = total[kCtrItems];
   for (;;) {
     const int t = queue_next(queue);
-    if (t >= *total) return;
-    const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
+    if (t >= n_items) return;
+    const PartRec pr = parts[t];
+    if (pr.vmode != 2) continue;
+    const int pidx = __builtin_amdgcn_readfirstlane(pr.pidx);
     const PageDev pg = pages[pidx];
     if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3) || pg.vmode != 2) continue;
     const JobDev job = jobs[pg.job];
@@ -428,8 +434,10 @@ __global__ void __launch_bounds__(64) k_str_count(JobDev* jobs, PageDev* pages, 
       } else {
         const HStream S = streams[pg.hs_val];
         const int serr = (S.status != kOK && S.produced < nn) ? S.status : kOK;
+        const bool last = pr.p + 1 >= pr.np;
+        const int64_t v_hi = last ? nn : (int64_t)parts[t + 1].v0;
         StrDictCount sk{gconst(job.dict_offs ? job.dict_offs : (const int64_t*)offs_arena), keys, dcount, nn, 0};
-        hybrid_expand(S, runs, blks, nn, sh, sk);
+        hybrid_expand(S, runs, blks, v_hi, sh, sk, pr.b0, last ? -1 : parts[t + 1].b0);
         const int64_t bad = wave_min(sk.bad);
         chars = wave_sum(sk.sum);
         if (bad < nn && (serr == kOK || bad < S.produced)) de = kDICT_INDEX;
@@ -441,9 +449,8 @@ __global__ void __launch_bounds__(64) k_str_count(JobDev* jobs, PageDev* pages, 
       de = kUNSUPPORTED;
     }
     if (lane == 0) {
-      PageDev& o = pages[pidx];
-      o.chars = chars;
-      if (de != kOK) o.decode_status = de;
+      parts[t].chars = chars;
+      if (de != kOK) atomicMin(&pages[pidx].decode_status, de);  // parts of a page: kDICT_INDEX wins
     }
   }
 }
@@ -805,22 +812,49 @@ __global__ void __launch_bounds__(64) k_str_dba(JobDev* jobs, PageDev* pages, co
 }
 
 // ---- K7c ---------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_char_scan(JobDev* jobs, PageDev* pages, int64_t* offs_arena) {
+// Per chunk: the chars of every part (dictionary parts: k_str_count; PLAIN
+// parts: from the page-relative value ends k_str_plain wrote; DELTA pages:
+// k_str_delta), an exclusive scan in part order -> each part's chunk char
+// offset (and a page's, its part 0's), the chunk's chars.  A PLAIN part also
+// keeps the page-relative start of its first value: k_str_copy rewrites the
+// ends in place, so a part cannot read its predecessor's last end then.
+__global__ void __launch_bounds__(256) k_char_scan(JobDev* jobs, PageDev* pages, PartRec* parts, int64_t* offs_arena) {
   __shared__ int64_t part[5];
   JobDev& job = jobs[blockIdx.x];
   if (job.value_width != 0 || job.status == kCAPACITY) return;
-  const int np = job.num_pages < job.page_cap ? job.num_pages : job.page_cap;
+  const int ni = job.n_items;
+  PartRec* pr = parts + job.item_base;
   int64_t carry = 0;
-  for (int b = 0; b < np; b += 256) {
+  for (int b = 0; b < ni; b += 256) {
     const int i = b + threadIdx.x;
-    int64_t v = 0;
-    if (i < np) {
-      const PageDev& pg = pages[job.page_base + i];
-      if ((pg.page_type == 0 || pg.page_type == 3) && pg.read_status == kOK && pg.decode_status == kOK) v = pg.chars;
+    int64_t v = 0, prel = 0;
+    int pidx = -1, p = 0;
+    if (i < ni) {
+      const PartRec r = pr[i];
+      pidx = r.pidx;
+      p = r.p;
+      const PageDev& pg = pages[pidx];
+      if ((pg.page_type == 0 || pg.page_type == 3) && pg.read_status == kOK && pg.decode_status == kOK &&
+          pg.vmode == 2) {
+        if (pg.encoding == 8) {
+          v = r.chars;
+        } else if (pg.encoding == 0) {
+          const PQG_G int64_t* ends = gconst(offs_arena) + job.offs_base + pg.value_offset + 1;
+          const int64_t lo = r.v0, hi = r.p + 1 < r.np ? (int64_t)pr[i + 1].v0 : (int64_t)pg.not_null;
+          prel = lo > 0 ? ends[lo - 1] : 0;
+          v = hi > lo ? ends[hi - 1] - prel : 0;
+        } else {
+          v = pg.chars;  // DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY: one part
+        }
+      }
     }
     int64_t tot;
     const int64_t ex = block_excl_scan<256>(v, &tot, part);
-    if (i < np) pages[job.page_base + i].char_offset = carry + ex;
+    if (i < ni) {
+      pr[i].cstart = carry + ex;
+      pr[i].prel = prel;
+      if (p == 0) pages[pidx].char_offset = carry + ex;
+    }
     carry += tot;
   }
   if (threadIdx.x == 0) {
@@ -842,35 +876,39 @@ namespace pqg {
 // entry `key`, and its start is a block scan of the entry lengths.  The ends
 // become chunk offsets.  512 independent copies per block keep many loads in
 // flight.
-__global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+__global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total,
                                                   int* queue, uint8_t* value_arena, int64_t* offs_arena) {
   __shared__ int s_t;
   __shared__ int64_t s_prev;  // page-relative end of the value before the round
   __shared__ int64_t part[9];
+  const int n_items = total[kCtrItems];
   for (;;) {
-    if (threadIdx.x == 0) {
-      s_t = queue_pull(queue);
-      s_prev = 0;
-    }
+    if (threadIdx.x == 0) s_t = queue_pull(queue);
     __syncthreads();
     const int t = s_t;
     __syncthreads();
-    if (t >= *total) return;
-    const int pidx = list[t];
+    if (t >= n_items) return;
+    const PartRec& pr = parts[t];
+    if (pr.vmode != 2) continue;
+    const int pidx = pr.pidx;
     const PageDev& pg = pages[pidx];
     if (pg.read_status != kOK || pg.decode_status != kOK || (pg.page_type != 0 && pg.page_type != 3) || pg.vmode != 2 ||
         pg.not_null == 0 || pg.encoding == 7)  // DELTA_BYTE_ARRAY: k_str_dba
       continue;
     const JobDev& job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
-    const int64_t nn = pg.not_null, base = pg.char_offset;
+    const int64_t base = pg.char_offset;
+    // the part's values [v_lo, nn): a page's part ends at the next part's first value
+    const int64_t v_lo = pr.v0, nn = pr.p + 1 < pr.np ? (int64_t)parts[t + 1].v0 : (int64_t)pg.not_null;
+    if (threadIdx.x == 0) s_prev = pg.encoding == 0 ? pr.prel : pg.encoding == 8 ? pr.cstart - base : 0;
+    __syncthreads();
     const bool dlba = pg.encoding == 6;  // value bytes back to back from cstart
     const gu8 chars = gmut(value_arena) + job.value_base + base;
     PQG_G int64_t* ends = gmut(offs_arena) + job.offs_base + pg.value_offset + 1;
     const bool dict = pg.encoding == 8;
     const gcu8 src = dict ? gconst(job.dict_data) : gconst(pg.val);
     const PQG_G int64_t* doffs = gconst(job.dict_offs);
-    for (int64_t i0 = 0; i0 < nn; i0 += 512) {
+    for (int64_t i0 = v_lo; i0 < nn; i0 += 512) {
       const int64_t i = i0 + threadIdx.x;
       int64_t e = 0, s0 = 0, from = 0;
       if (dict) {

@@ -694,38 +694,48 @@ union ValuesShared {
 
 // Mode 1: pages of 4-byte dictionary columns only (the C2 hot path, kept
 // apart so that its register budget is not the union of every encoding's);
-// mode 0: every other data page.  k_page_setup builds the two page lists.
+// mode 0: every other fixed-width page; mode 3: DELTA_BINARY_PACKED.  Work
+// items are the pages' parts (k_part_plan): a big page (parquet-go's writer: a
+// whole chunk in one page) is decoded by many waves, one part each.
 template <int Mode>
-__global__ void __launch_bounds__(64, Mode == 3 ? PQG_DBP_WPE : PQG_VALUES_WPE) k_values(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+__global__ void __launch_bounds__(64, Mode == 3 ? PQG_DBP_WPE : PQG_VALUES_WPE) k_values(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total,
                                                int* queue, uint8_t* value_arena, const HStream* streams,
                                                const RunEnt* runs, const BlockDesc* blks) {
   __shared__ __attribute__((aligned(16))) ValuesShared sh;
   const int lane = lane_id();
   if (total[kModePresentOff + Mode] == 0) return;  // no page of this stage
+  const int n_items = total[kCtrItems];
   for (;;) {
     PQG_T(tp0);
     const int t = queue_next(queue);
-    if (t >= *total) return;
-    // wave-uniform: page and job records are read once, by scalar loads, into
-    // locals (see k_levels_expand); results are written back at the end
-    const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
+    if (t >= n_items) return;
+    // wave-uniform: part, page and job records are read once, by scalar loads,
+    // into locals; results are written back at the end
+    const PartRec pr = parts[t];
+    if (pr.vmode != Mode) continue;
+    const int pidx = __builtin_amdgcn_readfirstlane(pr.pidx);
     const PageDev pg = pages[pidx];
     // every data page of the list is set up by k_page_levels, which also
     // chose its values stage (vmode)
     if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3) || pg.vmode != Mode) continue;
     const JobDev job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
+    const bool last = pr.p + 1 >= pr.np;
+    const uint32_t nx_v0 = last ? 0u : parts[t + 1].v0;
+    const int nx_b0 = last ? -1 : parts[t + 1].b0;
     const gcu8 val = gconst(pg.val);
     const int64_t vn = pg.val_n;
     // readable bytes from val (for wide loads)
     int64_t readable = (pg.scratch_offset >= 0) ? vn : job.data_len - (pg.val - job.data);
     const int enc = pg.encoding;
     const int64_t nn = pg.not_null;
+    // the part's values [v_lo, v_hi) (the whole page: [0, nn))
+    const int64_t v_lo = pr.v0, v_hi = last ? nn : (int64_t)nx_v0;
     PQG_T(tpa);
     PQG_ACC(10 + Mode, tp0, tpa);
     const int w = job.value_width;
     const gu8 out = gmut(value_arena) + job.value_base + pg.value_offset * (int64_t)w;
-    // ---- valuesDecoder.init (read phase)
+    // ---- valuesDecoder.init (read phase; every part finds the same)
     int re = kOK;
     int dict_w = 0;
     if ((Mode == 0 || Mode == 1) && enc == 8) {
@@ -750,20 +760,21 @@ __global__ void __launch_bounds__(64, Mode == 3 ? PQG_DBP_WPE : PQG_VALUES_WPE) 
       if (job.type == 0) {  // booleanPlainDecoder: one byte per 8 values
         if ((nn + 7) / 8 > vn) de = kEOF;
         else
-          for (int64_t i = lane; i < nn; i += 64) out[i] = (val[i >> 3] >> (i & 7)) & 1;
+          for (int64_t i = v_lo + lane; i < v_hi; i += 64) out[i] = (val[i >> 3] >> (i & 7)) & 1;
       } else if (job.type == 3) {  // INT96 (type_int96.go:21-42)
         int64_t full = vn / 12, rem = vn % 12;
         if (nn > full + (rem > 0 ? 1 : 0)) de = kEOF;
         else {
           // a partial final value is left nil (Q8): its bytes are zero
           const int64_t whole = nn < full ? nn : full;
-          if (nn == full + 1 && rem > 0 && lane == 0) pages[pidx].flags |= 1;
-          wave_copy(out, val, whole * 12);
-          if (whole < nn && lane < 12) out[whole * 12 + lane] = 0;
+          const int64_t w_hi = v_hi < whole ? v_hi : whole;
+          if (nn == full + 1 && rem > 0 && lane == 0 && whole >= v_lo && whole < v_hi) atomicOr(&pages[pidx].flags, 1);
+          if (w_hi > v_lo) wave_copy(out + v_lo * 12, val + v_lo * 12, (w_hi - v_lo) * 12);
+          if (whole >= v_lo && whole < v_hi && lane < 12) out[whole * 12 + lane] = 0;
         }
       } else if (w > 0) {  // INT32 / INT64 / FLOAT / DOUBLE / FLBA: little-endian bit copies
         if (nn * w > vn) de = kEOF;
-        else wave_copy(out, val, nn * w);
+        else wave_copy(out + v_lo * w, val + v_lo * w, (v_hi - v_lo) * w);
       } else {
         de = kUNSUPPORTED;  // variable length: pqg_strings.hip
       }
@@ -772,7 +783,7 @@ __global__ void __launch_bounds__(64, Mode == 3 ? PQG_DBP_WPE : PQG_VALUES_WPE) 
       const int64_t dcount = job.dict_data ? job.dict_count : 0;
       const int64_t nil_key = (job.flags & 1) ? dcount - 1 : -1;
       if (w == 0) {
-        de = kUNSUPPORTED;  // variable-length dictionaries: not in this build yet
+        de = kUNSUPPORTED;  // variable-length dictionaries: pqg_strings.hip
       } else if (dict_w == 0) {
         // a zero-width decoder yields key 0 forever, reading nothing (hybrid_decoder.go:84-86)
         if (dcount < 1) de = kDICT_INDEX;
@@ -783,19 +794,23 @@ __global__ void __launch_bounds__(64, Mode == 3 ? PQG_DBP_WPE : PQG_VALUES_WPE) 
         const int serr = (S.status != kOK && S.produced < nn) ? S.status : kOK;
         int64_t bad = nn;
         const gcu8 dsafe = dict ? dict : (gcu8)out;  // never dereferenced for a valid key when null
+        const int blo = pr.b0, bhi = nx_b0;
         if (Mode == 1 || w == 4) {
           DictSink<4> sk{out, dsafe, dcount, nn, nil_key, 4};
-          hybrid_expand(S, runs, blks, nn, sh.ex, sk);
+          hybrid_expand(S, runs, blks, v_hi, sh.ex, sk, blo, bhi);
           bad = wave_min(sk.bad);
         } else if (Mode == 0 && w == 8) {
           DictSink<8> sk{out, dsafe, dcount, nn, nil_key, 8};
-          hybrid_expand(S, runs, blks, nn, sh.ex, sk);
+          hybrid_expand(S, runs, blks, v_hi, sh.ex, sk, blo, bhi);
           bad = wave_min(sk.bad);
         } else if (Mode == 0) {
           DictSink<0> sk{out, dsafe, dcount, nn, nil_key, w};
-          hybrid_expand(S, runs, blks, nn, sh.ex, sk);
+          hybrid_expand(S, runs, blks, v_hi, sh.ex, sk, blo, bhi);
           bad = wave_min(sk.bad);
         }
+        // a bad key found lies before the stream's end (the expander stops
+        // there): "dict: invalid index" wins over the stream's own error
+        // (kDICT_INDEX is below kEOF / kRLE, so the parts' atomicMin agrees)
         if (bad < nn && (serr == kOK || bad < S.produced)) de = kDICT_INDEX;
         else de = serr;
       }
@@ -804,22 +819,22 @@ __global__ void __launch_bounds__(64, Mode == 3 ? PQG_DBP_WPE : PQG_VALUES_WPE) 
     } else if (Mode == 0 && enc == 3 && job.type == 0) {  // booleanRLEDecoder: hybrid w=1 after a u32 length
       const HStream S = streams[pg.hs_val];
       BoolSink sk{out};
-      hybrid_expand(S, runs, blks, nn, sh.ex, sk);
+      hybrid_expand(S, runs, blks, v_hi, sh.ex, sk, pr.b0, nx_b0);
       de = (S.status != kOK && S.produced < nn) ? S.status : kOK;
     } else {
       de = kUNSUPPORTED;
     }
-    if (lane == 0 && de != kOK) pages[pidx].decode_status = de;
+    if (lane == 0 && de != kOK) atomicMin(&pages[pidx].decode_status, de);
     PQG_T(tp1);
     PQG_ACC(8 + Mode, tp0, tp1);
   }
 }
 
-template __global__ void k_values<0>(JobDev*, PageDev*, const int*, const int*, int*, uint8_t*, const HStream*,
+template __global__ void k_values<0>(JobDev*, PageDev*, const PartRec*, const int*, int*, uint8_t*, const HStream*,
                                     const RunEnt*, const BlockDesc*);
-template __global__ void k_values<1>(JobDev*, PageDev*, const int*, const int*, int*, uint8_t*, const HStream*,
+template __global__ void k_values<1>(JobDev*, PageDev*, const PartRec*, const int*, int*, uint8_t*, const HStream*,
                                     const RunEnt*, const BlockDesc*);
-template __global__ void k_values<3>(JobDev*, PageDev*, const int*, const int*, int*, uint8_t*, const HStream*,
+template __global__ void k_values<3>(JobDev*, PageDev*, const PartRec*, const int*, int*, uint8_t*, const HStream*,
                                     const RunEnt*, const BlockDesc*);
 
 // ============================================================================
