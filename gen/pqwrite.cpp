@@ -516,7 +516,13 @@ ChunkOut write_chunk(Buf& file, const ColSpec& c, int64_t s0, int64_t s1, int64_
       hybrid_encode(vals, idx.data() + (vs - v0), nn, idx_w, c.min_rle, c.hybrid_groups);
       any_dict = true;
     } else if (enc == 6 || enc == 7) {
-      delta_byte_array(vals, c.values, c.offsets, vs, ve, enc == 7);
+      if (c.offsets) {
+        delta_byte_array(vals, c.values, c.offsets, vs, ve, enc == 7);
+      } else {  // FIXED_LEN_BYTE_ARRAY: values of type_length bytes
+        std::vector<int64_t> fo((size_t)(ve + 1));
+        for (int64_t i = 0; i <= ve; i++) fo[(size_t)i] = i * c.type_length;
+        delta_byte_array(vals, c.values, fo.data(), vs, ve, enc == 7);
+      }
     } else if (enc == 5) {
       if (c.type == 1)
         dbp_encode<int32_t>(vals, (const int32_t*)c.values + vs, nn);

@@ -89,6 +89,10 @@ enum {
   PQG_ERR_DICT_PAGE = -11,    /* second dictionary page                             */
   PQG_ERR_BYTE_ARRAY = -12,   /* bytearray/plain: negative length                   */
   PQG_ERR_LEVELS = -13,       /* level decoder not initialised (V2, zero length)    */
+  PQG_ERR_GZIP = -15,         /* gzip: invalid header / data / checksum (compress.go:63-76) */
+  PQG_ERR_FIXED_LEN = -14,    /* DELTA_BYTE_ARRAY on FIXED_LEN_BYTE_ARRAY: a value  */
+                              /* whose length is not type_length (the reference     */
+                              /* returns it; the fixed-width output cannot hold it) */
   PQG_ERR_CAPACITY = -20,     /* internal: arena too small; host grows and retries  */
   PQG_ERR_INVALID_ARG = -21,
   PQG_ERR_HIP = -22,

@@ -35,6 +35,8 @@ enum : int32_t {
   kDICT_PAGE = -11,
   kBYTE_ARRAY = -12,
   kLEVELS = -13,
+  kFIXED_LEN = -14,  // DELTA_BYTE_ARRAY on FLBA: a value of another length than type_length
+  kGZIP = -15,       // gzip: invalid header, DEFLATE data or checksum
   kCAPACITY = -20,
   kCOMPLEX = -30,   // internal: header needs the serial walk (deep thrift nesting)
 };

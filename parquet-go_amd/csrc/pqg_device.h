@@ -58,12 +58,12 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
 __device__ __forceinline__ int bits_len(uint32_t v) { return v ? 32 - __builtin_clz(v) : 0; }
 
-// getValuesDecoder chunk_reader.go:143-196 (DELTA_BYTE_ARRAY on FIXED_LEN_BYTE_ARRAY is outside this build)
+// getValuesDecoder chunk_reader.go:143-196
 __device__ __forceinline__ int values_supported(int type, int type_length, int enc) {
   switch (type) {
     case 0: return enc == 0 || enc == 3 || enc == 8;
     case 6: return enc == 0 || enc == 8 || enc == 6 || enc == 7;  // + DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY
-    case 7: return type_length >= 0 && (enc == 0 || enc == 8);
+    case 7: return type_length >= 0 && (enc == 0 || enc == 8 || enc == 7);  // chunk_reader.go:86-97
     case 3: case 4: case 5: return enc == 0 || enc == 8;
     case 1: case 2: return enc == 0 || enc == 5 || enc == 8;
   }

@@ -1119,10 +1119,11 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
       }
       // value-stage page lists: 4-byte dictionary pages (the hot path, a kernel
       // of its own), variable-length values (pqg_strings.hip) and everything else
-      const int vm = job.value_width == 0                            ? 2
-                     : (pg.encoding == 8 && job.value_width == 4) ? 1
-                     : pg.encoding == 5                           ? 3
-                                                                  : 0;
+      // (DELTA_BYTE_ARRAY on FLBA: the strings stage, values of type_length bytes)
+      const int vm = job.value_width == 0 || (pg.encoding == 7 && job.type == 7) ? 2
+                     : (pg.encoding == 8 && job.value_width == 4)                ? 1
+                     : pg.encoding == 5                                          ? 3
+                                                                                 : 0;
       P.vmode = vm;
       int* present = const_cast<int*>(total) + kModePresentOff;
       if (present[vm] == 0) present[vm] = 1;

@@ -223,6 +223,8 @@ const char* pqg_status_string(int s) {
     case PQG_ERR_DICT_PAGE: return "there should be only one dictionary";
     case PQG_ERR_BYTE_ARRAY: return "bytearray/plain: len is negative";
     case PQG_ERR_LEVELS: return "level reader is not initialized";
+    case PQG_ERR_FIXED_LEN: return "bytearray/delta: value length is not the fixed length";
+    case PQG_ERR_GZIP: return "gzip: invalid data";
     case PQG_ERR_CAPACITY: return "capacity";
     case PQG_ERR_INVALID_ARG: return "invalid argument";
     case PQG_ERR_HIP: return "HIP runtime error";
@@ -383,10 +385,14 @@ static int plan_batch(pqg_ctx* c) {
     d.blk_cap = bcap;
     d.blk_base = blk_total;
     blk_total += bcap;
-    if (d.value_width == 0) {
+    // offsets: variable-length values; FLBA columns too (their DELTA_BYTE_ARRAY
+    // pages park prefix / suffix lengths there, k_str_delta)
+    if (d.value_width == 0 || d.type == PQG_FIXED_LEN_BYTE_ARRAY) {
       d.offs_cap = scap + 1;
       d.offs_base = offs_total;
       offs_total += align_up(scap + 1, 32);
+    }
+    if (d.value_width == 0) {
       // dictionary entries take >= 4 bytes each
       int64_t dcap = std::min<int64_t>(std::max<int64_t>(in.total_uncompressed_size, 0) / 4, 1 << 17) + 64;
       if (f.doffs > 0) dcap = f.doffs;
@@ -609,7 +615,8 @@ int pqg_decode_chunks_async(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs) {
   for (int i = 0; i < n_jobs; i++) {
     auto it = c->learned.find(JobKey{(uintptr_t)jobs[i].data, jobs[i].total_compressed_size, jobs[i].num_values_hint});
     if (it != c->learned.end()) c->force[(size_t)i] = it->second;
-    c->any_var |= value_width_of(jobs[i].col) == 0;
+    // the strings stage: variable-length columns, and FLBA (DELTA_BYTE_ARRAY pages)
+    c->any_var |= value_width_of(jobs[i].col) == 0 || jobs[i].col.physical_type == PQG_FIXED_LEN_BYTE_ARRAY;
     // k_values<0>: every fixed-width column but 4-byte ones with only dictionary pages
     c->any_fixed_other |= value_width_of(jobs[i].col) != 0;
   }

@@ -683,6 +683,7 @@ __global__ void __launch_bounds__(64) k_str_delta(JobDev* jobs, PageDev* pages, 
           else if (cs + my_send > vn) ve = kEOF;                 // io.ReadFull: "there is no byte left"
           else if (dba && (int64_t)pl + sl < 0) ve = kBYTE_ARRAY; // negative capacity
           else if (dba && prev_l < (int64_t)pl) ve = kBYTE_ARRAY; // "invalid prefix len in the stream"
+          else if (job.value_width > 0 && my_len != job.value_width) ve = kFIXED_LEN;  // FLBA: DESIGN.md
         }
         if (live && ve == kOK)
           slots[i] = dba ? (int64_t)(((uint64_t)eff_pl << 32) | (uint64_t)(uint32_t)my_send) : my_send;
@@ -735,7 +736,9 @@ __global__ void __launch_bounds__(64) k_str_dba(JobDev* jobs, PageDev* pages, co
       continue;
     const JobDev job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
-    const int64_t nn = pg.not_null, base = pg.char_offset;
+    // FLBA (fixed width): value i at (value_offset + i) * type_length, no offsets out
+    const bool fixed = job.value_width > 0;
+    const int64_t nn = pg.not_null, base = fixed ? pg.value_offset * job.value_width : pg.char_offset;
     const gu8 chars = gmut(value_arena) + job.value_base + base;
     PQG_G int64_t* slots = gmut(offs_arena) + job.offs_base + pg.value_offset + 1;
     const gcu8 suf = gconst(pg.val) + pg.cstart;
@@ -757,7 +760,7 @@ __global__ void __launch_bounds__(64) k_str_dba(JobDev* jobs, PageDev* pages, co
       int64_t incl;
       const int64_t ex = wave_excl_scan_i64(len, &incl);
       const int64_t ostart = oend + ex;
-      if (i < nn) slots[i] = base + ostart + len;
+      if (i < nn && !fixed) slots[i] = base + ostart + len;
       const int nv = (int)(nn - i0 < 64 ? nn - i0 : 64);
       const int64_t g_ss = sprev, g_se = __shfl(se, nv - 1, 64);
       // the group's suffixes into LDS (when they fit)

@@ -32,6 +32,8 @@ STATUS = {
     -11: "DICT_PAGE",
     -12: "BYTE_ARRAY",
     -13: "LEVELS",
+    -14: "FIXED_LEN",
+    -15: "GZIP",
     -20: "CAPACITY",
     -21: "INVALID_ARG",
     -22: "HIP",

@@ -134,12 +134,61 @@ def test_oracle_hand_pages(case):
         assert len(got) == 9 and got[1][:2] == got[0][:2]
 
 
-def test_flba_delta_byte_array_unsupported():
-    """DELTA_BYTE_ARRAY on FIXED_LEN_BYTE_ARRAY (chunk_reader.go:90-91) is not
-    built: both paths report UNSUPPORTED."""
-    chunk = _page_chunk(_dba([0, 1, 1, 0, 1, 1, 0, 2, 2], [4] * 9, bytes(36)), 9, DBA)
-    job, _ = U.chunk_job(chunk, ptype=abi.FIXED_LEN_BYTE_ARRAY, type_length=4)
-    assert O.decode_chunk(job).status == abi.STATUS_CODES["UNSUPPORTED"]
+def flba_cases():
+    """DELTA_BYTE_ARRAY on FIXED_LEN_BYTE_ARRAY (getFixedLenByteArrayValuesDecoder
+    chunk_reader.go:90-91 -> byteArrayDeltaDecoder type_bytearray.go:189-240):
+    (name, chunk, type_length, expected status).  Values of type_length bytes
+    decode into the fixed-width output; a value of another length (which the
+    reference would hand out as is) fails the page with FIXED_LEN."""
+    # 9 values of 4 bytes: prefixes shared with the previous value
+    pre = [0, 1, 1, 0, 4, 2, 0, 3, 3]
+    suf = [4 - p for p in pre]
+    chars = bytes(range(65, 65 + sum(suf)))
+    bad_suf = list(suf)
+    bad_suf[5] += 1
+    return [
+        ("flba_dba_ok", _page_chunk(_dba(pre, suf, chars), 9, DBA), 4, 0),
+        ("flba_dba_len", _page_chunk(_dba(pre, bad_suf, chars + b"x"), 9, DBA), 4, abi.STATUS_CODES["FIXED_LEN"]),
+        # the reference's own errors come first in value order
+        ("flba_dba_prefix", _page_chunk(_dba([0, 1, 9, 0, 4, 2, 0, 3, 3], suf, chars), 9, DBA), 4,
+         abi.STATUS_CODES["BYTE_ARRAY"]),
+        ("flba_dba_tl0", _page_chunk(_dba(pre, bad_suf, chars + b"x"), 9, DBA), 0, 0),  # length 0: byte arrays
+    ]
+
+
+@pytest.mark.parametrize("case", flba_cases(), ids=lambda c: c[0])
+def test_oracle_flba_delta_byte_array(case):
+    name, chunk, tl, want = case
+    job, _ = U.chunk_job(chunk, ptype=abi.FIXED_LEN_BYTE_ARRAY, type_length=tl)
+    r = O.decode_chunk(job)
+    assert r.status == want, "%s: %s" % (name, abi.status_name(r.status))
+    if name == "flba_dba_ok":
+        v = np.asarray(r.values).reshape(9, 4)
+        assert bytes(v[1][:1]) == bytes(v[0][:1]) and bytes(v[4]) == bytes(v[3])
+
+
+def test_oracle_flba_generated():
+    """A generated FLBA(6) column written with DELTA_BYTE_ARRAY (prefixes
+    shared with the previous value), nulls included: the oracle returns the
+    generator's values, densely."""
+    import pqgpu
+    data, vals = _flba_file()
+    pf = pqgpu.ParquetFile(data)
+    r = O.decode_chunk(pf.host_job(0, 0)[0])
+    assert r.status == 0, abi.status_name(r.status)
+    assert r.value_width == 6 and np.array_equal(np.asarray(r.values), vals)
+
+
+def _flba_file(rows=20000):
+    rng = np.random.default_rng(21)
+    defs = (rng.random(rows) >= 0.1).astype(np.uint8)
+    nn = int(defs.sum())
+    base = rng.integers(65, 91, size=(nn, 6)).astype(np.uint8)
+    base[:, :3] = base[np.sort(rng.integers(0, nn, nn)), :3]  # shared prefixes
+    vals = np.ascontiguousarray(base[np.lexsort(base.T[::-1])]).reshape(-1)
+    col = W.Column("fx", W.FLBA, vals, type_length=6, repetition=W.OPTIONAL, def_levels=defs, encoding=DBA,
+                   rows_per_page=3000)
+    return W.write_file([col], rows), vals
 
 
 # ---------------------------------------------------------------- GPU vs oracle
@@ -215,3 +264,15 @@ def test_gpu_mutations(dec):
             for _ in range(int(rng.integers(1, 4))):
                 b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
             P.compare_chunk_bytes(bytes(b), dec, ptype=abi.BYTE_ARRAY, max_def=d.max_def)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", flba_cases(), ids=lambda c: c[0])
+def test_gpu_flba_hand_pages(dec, case):
+    P.compare_chunk_bytes(case[1], dec, ptype=abi.FIXED_LEN_BYTE_ARRAY, type_length=case[2])
+
+
+@pytest.mark.gpu
+def test_gpu_flba_generated(dec):
+    data, _ = _flba_file()
+    P.compare_file(data, dec)
