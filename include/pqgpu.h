@@ -246,9 +246,11 @@ int pqg_decode_page(pqg_ctx* ctx, const pqg_page_job* job, pqg_chunk_result* res
 /* BlockCompressor.DecompressBlock (compress.go:24-27, 46-48, registered with
  * RegisterBlockCompressor compress.go:124-135): decompress one HOST block
  * synchronously on the GPU.  codec SNAPPY (snappy.Decode semantics: decoded
- * length from the block's varint header, ErrCorrupt -> PQG_ERR_SNAPPY) or
- * UNCOMPRESSED (a copy); GZIP -> PQG_ERR_UNSUPPORTED.  *out_len is the decoded
- * length; PQG_ERR_CAPACITY when it exceeds `cap` (nothing written). */
+ * length from the block's varint header, ErrCorrupt -> PQG_ERR_SNAPPY), GZIP
+ * (gzipCompressor.DecompressBlock, compress.go:63-76: multistream members,
+ * a bad header / block / CRC / ISIZE or trailing bytes -> PQG_ERR_GZIP) or
+ * UNCOMPRESSED (a copy).  *out_len is the decoded length; PQG_ERR_CAPACITY
+ * when it exceeds `cap` (nothing written). */
 int pqg_block_decompress(pqg_ctx* ctx, int codec, const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap,
                          int64_t* out_len);
 

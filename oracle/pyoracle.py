@@ -41,6 +41,7 @@ def lib():
         L.pqo_unpack8_64.argtypes = [C.c_char_p, C.c_int, C.c_void_p]
         L.pqo_hybrid_decode.argtypes = [C.c_char_p, C.c_int64, C.c_int, C.c_int64, C.c_void_p]
         L.pqo_snappy_decode.argtypes = [C.c_char_p, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
+        L.pqo_gzip_decode.argtypes = [C.c_char_p, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
         L.pqo_delta_decode64.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_void_p]
         L.pqo_delta_decode32.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_void_p]
         L.pqo_assemble.argtypes = [C.POINTER(abi.AssembleArgs)]
@@ -72,6 +73,13 @@ def snappy_decode(src: bytes, cap: int = 1 << 26):
     dst = np.zeros(max(cap, 1), dtype=np.uint8)
     n = C.c_int64(0)
     rc = lib().pqo_snappy_decode(bytes(src), len(src), dst.ctypes.data, cap, C.byref(n))
+    return rc, dst[: n.value].tobytes() if rc == 0 else b""
+
+
+def gzip_decode(src: bytes, cap: int = 1 << 26):
+    dst = np.zeros(max(cap, 1), dtype=np.uint8)
+    n = C.c_int64(0)
+    rc = lib().pqo_gzip_decode(bytes(src), len(src), dst.ctypes.data, cap, C.byref(n))
     return rc, dst[: n.value].tobytes() if rc == 0 else b""
 
 

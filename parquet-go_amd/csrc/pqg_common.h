@@ -85,7 +85,10 @@ struct PageDev {
   // compressed segments, and the serial-fallback flag (non-zero: k_snappy
   // decodes the page as one block)
   int32_t sn_hdr, sn_nsub, sn_sub_base, sn_nseg, sn_seg_base, sn_fallback;
+  int64_t gz_len;          // K2g (pqg_inflate.hip), bare blocks: decoded bytes
 };
+constexpr int32_t kPageBareBlock = 1 << 4;  // PageDev.flags: a pqg_block_decompress block (no page around it)
+constexpr int32_t kCodecSnappy = 1, kCodecGzip = 2;
 
 // K2 snappy sub-block: the output [j * kSnapSub, (j + 1) * kSnapSub) of one
 // compressed block, decoded by one wave from a chain tag at or before its
@@ -287,7 +290,8 @@ constexpr int kQueueSnapSerial = 10;
 constexpr int kQueueStrDelta = 11;
 constexpr int kQueueStrDba = 12;
 constexpr int kQueueLevLong = 13;  // pieces of the long level runs (k_level_long)
-constexpr int kQueueSlots = 14;  // queue regions zeroed per launch: 0-8, the stage flags (9), 10-13
+constexpr int kQueueInflate = 14;  // GZIP pages (k_inflate)
+constexpr int kQueueSlots = 15;  // queue regions zeroed per launch: 0-8, the stage flags (9), 10-14
 
 // Scan tiles of the speculative page-header search.
 constexpr int kScanTile = 16384;

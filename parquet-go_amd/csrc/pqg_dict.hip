@@ -48,17 +48,12 @@ constexpr int kPBlocks = 63;            // blocks per piece (lane 63's descripto
 #endif
 constexpr int kPRuns = PQG_DICT_PRUNS;   // run entries per piece (a multiple of 128)
 constexpr int kPPay = PQG_DICT_PPAY;    // payload bytes per piece
-#ifndef PQG_DICT_FLUSH
-#define PQG_DICT_FLUSH 1
-#endif
-constexpr int kFlushBlocks = PQG_DICT_FLUSH;  // blocks decoded into obuf per flush
 constexpr int kPG = kPPay / 1024;       // payload granules per lane
 constexpr int kPRunGr = kPRuns / 128;   // run-table granules per lane
 
 struct PieceShared {
   RunEnt runs[kPRunGr * 128];       // from the 16-byte granule holding the piece's first run
   uint32_t stage[kPG * 256 + 4];    // payload window from a 16-byte aligned address (+ a dword past it)
-  uint32_t obuf[kFlushBlocks * kHBlock + 8];  // values of the blocks of a flush (+ <= 3 dwords carried), see OutState
   uint8_t rmap[kHBlock];            // run starting at each value of a multi-run block
   uint8_t ridx[kHBlock];            // run of each value of a multi-run block
 };
@@ -135,26 +130,15 @@ struct GlobalDict {
   __device__ __forceinline__ uint32_t operator()(uint32_t k) const { return d[k]; }
 };
 
-// Per-wave output state of a page: values go through the wave's LDS buffer
-// `obuf` so that every global store is a whole aligned 16-byte granule, 64
-// consecutive granules (1 KiB) per store instruction, whatever the page's
-// alignment.  obuf[0, carry) holds the dwords of the granule at `gaddr` that
-// were not stored yet.
-struct OutState {
-  uintptr_t first;  // address of the page's value 0
-  uintptr_t gaddr;  // address of obuf[0] (16-byte aligned)
-  uint32_t carry;   // dwords pending in obuf[0, carry)
-};
-
-// Keys of block B (lane L: values L + 64 q, q < 8, so that LDS writes and reads
-// of consecutive values are conflict-free), looked up, written to
-// obuf[obase + value - B.v0].  `bad`: first value index with key >= dcount.
+// Keys of block B (lane L: values L + 64 q, q < 8: the LDS reads of the run
+// marks are conflict-free, and each store instruction writes 64 consecutive
+// values, 256 contiguous bytes), looked up and stored to out[value - B.v0]
+// (out: the block's first value).  `bad`: first value index with key >= dcount.
 template <class Dict>
-__device__ __forceinline__ void block_to_obuf(PieceShared& ps, const PBlock& B, uint32_t mask, int w, int64_t plo8,
-                                              int lane, uint32_t obase, uint32_t dcount, const Dict& dict,
-                                              int64_t& bad) {
+__device__ __forceinline__ void block_out(PieceShared& ps, const PBlock& B, uint32_t mask, int w, int64_t plo8,
+                                          int lane, PQG_G uint32_t* out, uint32_t dcount, const Dict& dict,
+                                          int64_t& bad) {
   const uint32_t nv = B.v1 - B.v0;  // <= kHBlock
-  PQG_L uint32_t* ob = lds_ptr(ps.obuf) + obase;
   uint32_t key[8];
   if (B.nr == 1) {
     const RunEnt e = ps.runs[B.rl];
@@ -165,7 +149,7 @@ __device__ __forceinline__ void block_to_obuf(PieceShared& ps, const PBlock& B, 
       if (src >= dcount) bad = (int64_t)B.v0 < bad ? (int64_t)B.v0 : bad;
 #pragma unroll
       for (int q = 0; q < 8; q++)
-        if ((uint32_t)(lane + 64 * q) < nv) ob[lane + 64 * q] = x;
+        if ((uint32_t)(lane + 64 * q) < nv) out[lane + 64 * q] = x;
       return;
     }
     const uint32_t rb0 = (uint32_t)((int64_t)src * 8 - plo8) + (B.v0 + (uint32_t)lane - (st & ~kRunBP)) * (uint32_t)w;
@@ -207,7 +191,7 @@ __device__ __forceinline__ void block_to_obuf(PieceShared& ps, const PBlock& B, 
       key[q] = (e.start & kRunBP) ? bits : e.src;
     }
   }
-  // every lookup of the block issued before the first write
+  // every lookup of the block issued before the first store
   uint32_t mx = 0;
 #pragma unroll
   for (int q = 0; q < 8; q++) mx = (uint32_t)(lane + 64 * q) < nv && key[q] > mx ? key[q] : mx;
@@ -224,53 +208,11 @@ __device__ __forceinline__ void block_to_obuf(PieceShared& ps, const PBlock& B, 
   for (int q = 0; q < 8; q++) val[q] = dict((uint32_t)(lane + 64 * q) < nv ? key[q] : 0u);
 #pragma unroll
   for (int q = 0; q < 8; q++)
-    if ((uint32_t)(lane + 64 * q) < nv) ob[lane + 64 * q] = val[q];
+    if ((uint32_t)(lane + 64 * q) < nv) out[lane + 64 * q] = val[q];
 }
 
-// Store obuf[0, total) (dwords from os.gaddr) as whole granules; keep the
-// ragged tail in obuf[0, carry).  Dwords before the page's first value belong
-// to another page: the page's first granule is stored dword by dword.
-__device__ __forceinline__ void flush_obuf(PieceShared& ps, OutState& os, uint32_t total, int lane) {
-  __builtin_amdgcn_wave_barrier();
-  const uint32_t full = total >> 2;
-  const PQG_L u32x4_t* ob4 = (const PQG_L u32x4_t*)lds_ptr(ps.obuf);
-#pragma unroll
-  for (int k = 0; k < (kFlushBlocks * kHBlock + 4) / 256 + 1; k++) {
-    const uint32_t g = (uint32_t)(lane + 64 * k);
-    if (g < full) {
-      const u32x4_t x = ob4[g];
-      const uintptr_t a = os.gaddr + 16 * (uintptr_t)g;
-      if (a >= os.first) {
-        *(PQG_G u32x4_t*)a = x;
-      } else {
-        if (a + 4 >= os.first) *(PQG_G uint32_t*)(a + 4) = x.y;
-        if (a + 8 >= os.first) *(PQG_G uint32_t*)(a + 8) = x.z;
-        *(PQG_G uint32_t*)(a + 12) = x.w;  // the first value is in this granule: dword 3 is the page's
-      }
-    }
-  }
-  const uint32_t rem = total & 3;
-  uint32_t t = 0;
-  if ((uint32_t)lane < rem) t = ps.obuf[4 * full + lane];
-  __builtin_amdgcn_wave_barrier();
-  if ((uint32_t)lane < rem) ps.obuf[lane] = t;
-  __builtin_amdgcn_wave_barrier();
-  os.gaddr += 16 * (uintptr_t)full;
-  os.carry = rem;
-}
-
-// The pending dwords at the end of the page.
-__device__ __forceinline__ void flush_tail(PieceShared& ps, OutState& os, int lane) {
-  __builtin_amdgcn_wave_barrier();
-  if ((uint32_t)lane < os.carry) {
-    const uintptr_t a = os.gaddr + 4 * (uintptr_t)lane;
-    if (a >= os.first) *(PQG_G uint32_t*)a = ps.obuf[lane];
-  }
-  os.carry = 0;
-}
-
-// Decode one page: keys piece by piece, looked up in `dict`, stored through
-// obuf.  A piece is one round of independent loads: the descriptors of blocks
+// Decode one page (or a part of a big page): keys piece by piece, looked up
+// in `dict`, stored straight to `out` (the first block's value 0).  A piece is one round of independent loads: the descriptors of blocks
 // kb .. kb + 63, kPRuns run entries from the run of block kb, and a kPPay-byte
 // payload window from `pos` (at or before the next payload byte the page
 // needs: blocks consume the stream in order, and a block's payload starts at
@@ -286,16 +228,14 @@ __device__ __forceinline__ int64_t dict_page(PieceShared& ps, const gcu8 sp, con
   int64_t bad = INT64_MAX;
   if (end_all == 0) return bad;
   const uintptr_t pa = (uintptr_t)sp;
-  OutState os;
-  os.first = (uintptr_t)out;
-  os.gaddr = os.first & ~(uintptr_t)15;
-  os.carry = (uint32_t)((os.first - os.gaddr) >> 2);
   if (nb_all <= 0) return bad;
   int kb = 0;
   // a part of a big page starts at any block: its first run and payload byte
   const uint4 d0 = ldg16((uintptr_t)blks);
   uint32_t rcur = d0.y;                 // first run of block kb
   int64_t pos = (d0.w & 0xffffu) ? (int64_t)d0.z : 0;  // stream offset of the payload window (before alignment)
+  const uint32_t vfirst = d0.x;         // the first block's value 0: out[0]
+  PQG_G uint32_t* const out32 = (PQG_G uint32_t*)out;
   while (kb < nb_all) {
     PQG_DT(ta);
     // ---- one round of loads: descriptors, run entries, payload window
@@ -342,29 +282,19 @@ __device__ __forceinline__ int64_t dict_page(PieceShared& ps, const gcu8 sp, con
       continue;
     }
     const int64_t plo8 = plo * 8;
-    // ---- blocks of the piece, kFlushBlocks per flush
-    for (int k0 = 0; k0 < m; k0 += kFlushBlocks) {
+    // ---- blocks of the piece
+    for (int k = 0; k < m; k++) {
       PQG_DT(tp0);
-      uint32_t tot = os.carry;
-#pragma unroll
-      for (int b = 0; b < kFlushBlocks; b++) {
-        if (k0 + b >= m) break;
-        const int k = k0 + b;
-        PBlock B;
-        B.on = true;
-        B.v0 = (uint32_t)__builtin_amdgcn_readlane((int)v0, k);
-        const uint32_t nx = (uint32_t)__builtin_amdgcn_readlane((int)v0, k + 1);
-        B.v1 = nx < end_all ? nx : end_all;
-        B.rl = (uint32_t)__builtin_amdgcn_readlane((int)r0, k) - rcur + (uint32_t)rskew;
-        B.nr = (uint32_t)__builtin_amdgcn_readlane((int)nr, k);
-        block_to_obuf(ps, B, mask, w, plo8, lane, tot, dcount, dict, bad);
-        tot += B.v1 - B.v0;
-      }
+      PBlock B;
+      B.on = true;
+      B.v0 = (uint32_t)__builtin_amdgcn_readlane((int)v0, k);
+      const uint32_t nx = (uint32_t)__builtin_amdgcn_readlane((int)v0, k + 1);
+      B.v1 = nx < end_all ? nx : end_all;
+      B.rl = (uint32_t)__builtin_amdgcn_readlane((int)r0, k) - rcur + (uint32_t)rskew;
+      B.nr = (uint32_t)__builtin_amdgcn_readlane((int)nr, k);
+      block_out(ps, B, mask, w, plo8, lane, out32 + (B.v0 - vfirst), dcount, dict, bad);
       PQG_DT(tp2);
-      flush_obuf(ps, os, tot, lane);
-      PQG_DT(tp3);
       pf.add(11, tp2 - tp0);
-      pf.add(12, tp3 - tp2);
     }
     __builtin_amdgcn_wave_barrier();
     PQG_DT(tc);
@@ -379,7 +309,6 @@ __device__ __forceinline__ int64_t dict_page(PieceShared& ps, const gcu8 sp, con
     if (nxp) pos = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, __builtin_ctzll(nxp));
     else if (phi > 0) pos = (int64_t)phi - 1;
   }
-  flush_tail(ps, os, lane);
   return bad;
 }
 

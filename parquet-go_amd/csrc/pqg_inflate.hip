@@ -1,0 +1,553 @@
+// pqg_inflate.hip — GZIP pages: gzipCompressor.DecompressBlock (compress.go:63-76):
+// gzip.NewReader + ioutil.ReadAll over the page's compressed block, i.e. Go's
+// compress/gzip in its default multistream mode (RFC 1952 members, one after
+// another, until the block ends exactly after one) around compress/flate
+// (RFC 1951).  The decoded bytes of a valid stream are the format's; errors
+// (bad header, bad DEFLATE data, CRC-32 / ISIZE mismatch, a truncated member,
+// trailing bytes that are not a member) are PQG_ERR_GZIP, as the oracle
+// classifies them (oracle/pq_oracle.cpp gzip_decode); a decoded length other
+// than the page's uncompressed size is PQG_ERR_SIZE (compress.go:117).
+//
+// One wave per compressed page.  DEFLATE is a serial bit stream, so the
+// symbol decode runs wave-uniform (every lane holds the same decoder state;
+// table reads are LDS broadcasts) with canonical-Huffman tables built per
+// block in LDS (a 9-bit fast table, then the count / symbol walk of RFC 1951
+// codes); the lanes split the byte work: copies of a match from the 32 KiB
+// LDS history ring, the table builds, the flush of decoded bytes to HBM in
+// 16-byte granules, and the CRC-32 of every flushed piece (per-lane slices
+// combined in a tree with x^(8n) mod P shifts).
+#include <hip/hip_runtime.h>
+
+#include "pqg_common.h"
+#include "pqg_device.h"
+#include "pqg_hybrid.h"
+
+namespace pqg {
+
+namespace {
+
+constexpr int kRing = 32768;      // DEFLATE window: the whole history a distance can reach
+constexpr int kInStage = 1024;    // compressed bytes staged in LDS per refill
+constexpr int kFlush = 16384;     // decoded bytes flushed (and CRC'd) at a time
+constexpr int kFastBits = 9;
+constexpr uint32_t kCrcPoly = 0xedb88320u;  // CRC-32 (IEEE, reflected): gzip trailer
+
+struct Huff {
+  uint16_t count[16];    // codes per length
+  uint16_t symbol[288];  // symbols by (length, value)
+  uint16_t fast[1 << kFastBits];  // next 9 stream bits -> (length << 9) | symbol, 0: longer code
+};
+
+struct InflateShared {
+  uint8_t ring[kRing];
+  uint8_t in[kInStage + 16];
+  uint32_t crc_tab[256];
+  uint32_t seg_crc[64];
+  Huff lit, dist;
+  uint16_t lens[352];  // code lengths: [0, 19) code-length code, [32, 348) decoded, then lit/len [0, 286) + dist [288, 318)
+  int err;  // table build errors (any lane)
+};
+
+__device__ const uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                          31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__device__ const uint8_t kLenExt[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__device__ const uint16_t kDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
+                                           193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__device__ const uint8_t kDistExt[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__device__ const uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// a * b mod P over GF(2), reflected (bit 31 = x^0): zlib's multmodp
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = b & 1 ? (b >> 1) ^ kCrcPoly : b >> 1;
+  }
+  return p;
+}
+// x^(8 n) mod P
+__device__ __forceinline__ uint32_t x8nmodp(uint64_t n) {
+  uint32_t p = 1u << 31;       // x^0
+  uint32_t sq = 1u << 23;      // x^8
+  while (n) {
+    if (n & 1) p = multmodp(sq, p);
+    n >>= 1;
+    sq = multmodp(sq, sq);
+  }
+  return p;
+}
+
+}  // namespace
+
+// One wave's inflater.  Every lane holds the same state (wave-uniform control
+// flow); `lane` splits the byte-parallel steps.
+struct Inflater {
+  InflateShared* sh;
+  gcu8 src;
+  int64_t n;            // compressed bytes
+  int64_t pos = 0;      // next byte for the bit buffer
+  int64_t in_base = -(int64_t)kInStage * 4;  // stream offset of in[0]
+  uint64_t bitbuf = 0;
+  int bitcnt = 0;
+  gu8 dst;              // decoded bytes (cap of them are stored)
+  int64_t cap;
+  int64_t d = 0;        // decoded bytes so far
+  int64_t flushed = 0;  // decoded bytes flushed (stored and CRC'd)
+  int64_t mstart = 0;   // first decoded byte of the current member
+  uint32_t crc = 0;     // CRC-32 of the member's flushed bytes (conditioned)
+  int lane;
+
+  __device__ void stage(int64_t at) {
+    // 16-byte granules from the aligned address at or below `at`; granules
+    // past the block re-read its last one (never used)
+    const uintptr_t a0 = (uintptr_t)(src + at) & ~(uintptr_t)15;
+    in_base = at - (int64_t)((uintptr_t)(src + at) - a0);
+    const uintptr_t last = ((uintptr_t)(src + n) - 1) & ~(uintptr_t)15;
+    const uintptr_t a = a0 + 16 * (uintptr_t)lane;
+    const uint4 v = ldg16(a <= last ? a : last);
+    __builtin_amdgcn_wave_barrier();
+    sts16(lds_ptr(sh->in) + 16 * lane, v);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ __forceinline__ int byte_at(int64_t i) {
+    if (i < in_base || i >= in_base + kInStage) stage(i);
+    return lds_ptr(sh->in)[i - in_base];
+  }
+  // at least k (<= 32) bits in the buffer; false past the end of the block
+  __device__ __forceinline__ bool need(int k) {
+    while (bitcnt < k) {
+      if (pos >= n) return false;
+      bitbuf |= (uint64_t)(uint32_t)byte_at(pos) << bitcnt;
+      pos++;
+      bitcnt += 8;
+    }
+    return true;
+  }
+  __device__ __forceinline__ bool bits(int k, uint32_t* v) {
+    if (k == 0) { *v = 0; return true; }
+    if (!need(k)) return false;
+    *v = (uint32_t)bitbuf & ((1u << k) - 1);
+    bitbuf >>= k;
+    bitcnt -= k;
+    return true;
+  }
+  // the bytes of the next whole byte boundary on (stored blocks, trailers)
+  __device__ __forceinline__ void align_byte() {
+    const int r = bitcnt & 7;
+    bitbuf >>= r;
+    bitcnt -= r;
+  }
+  __device__ __forceinline__ bool byte_aligned(uint32_t* v) { return bits(8, v); }
+
+  // Canonical code from lengths[0..n) (RFC 1951 3.2.2): counts, symbols, and
+  // the 9-bit fast table.  Returns the number of unused code points at the
+  // longest length (< 0: over-subscribed, 0: complete, > 0: incomplete), as
+  // puff's construct.
+  __device__ int build(Huff& h, const uint16_t* lengths, int nsym) {
+    PQG_L Huff* H = lds_ptr(&h);
+    // counts (every lane, the same: n <= 288, cheap next to the block's symbols)
+    uint32_t cnt[16];
+#pragma unroll
+    for (int l = 0; l < 16; l++) cnt[l] = 0;
+    for (int s = 0; s < nsym; s++) {
+      const uint32_t L = lds_ptr(lengths)[s];
+#pragma unroll
+      for (int l = 0; l < 16; l++) cnt[l] += L == (uint32_t)l;
+    }
+    int left = 1;
+    for (int l = 1; l < 16; l++) {
+      left <<= 1;
+      left -= (int)cnt[l];
+    }
+#pragma unroll
+    for (int l = 0; l < 16; l++)
+      if (lane == l) H->count[l] = (uint16_t)cnt[l];
+    // symbols by length then value: symbol s of length L goes after every
+    // shorter code and every smaller symbol of length L
+    for (int s = lane; s < nsym; s += 64) {
+      const uint32_t L = lds_ptr(lengths)[s];
+      if (L == 0) continue;
+      uint32_t at = 0;
+#pragma unroll
+      for (int l = 1; l < 16; l++) at += (uint32_t)l < L ? cnt[l] : 0u;
+      for (int t = 0; t < s; t++) at += lds_ptr(lengths)[t] == L;
+      H->symbol[at] = (uint16_t)s;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // fast table: entry x = the next 9 stream bits (LSB first)
+    for (int x = lane; x < (1 << kFastBits); x += 64) {
+      int code = 0, first = 0, index = 0;
+      uint16_t e = 0;
+      for (int l = 1; l <= kFastBits; l++) {
+        code |= (x >> (l - 1)) & 1;
+        const int c = (int)cnt[l];
+        if (code - c < first) {
+          e = (uint16_t)(l << 9 | H->symbol[index + (code - first)]);
+          break;
+        }
+        index += c;
+        first += c;
+        first <<= 1;
+        code <<= 1;
+      }
+      H->fast[x] = e;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return left;
+  }
+
+  // next symbol of code h, or -1 (out of input, or no such code)
+  __device__ __forceinline__ int decode(const Huff& h) {
+    const PQG_L Huff* H = lds_ptr(&h);
+    need(kFastBits);  // as many as the block holds
+    if (bitcnt >= kFastBits || bitcnt > 0) {
+      const uint32_t e = H->fast[(uint32_t)bitbuf & ((1u << kFastBits) - 1)];
+      const int l = (int)(e >> 9);
+      if (e != 0 && l <= bitcnt) {
+        bitbuf >>= l;
+        bitcnt -= l;
+        return (int)(e & 511);
+      }
+    }
+    // the slow walk, bit by bit (codes longer than 9 bits, or the block's end)
+    int code = 0, first = 0, index = 0;
+    for (int l = 1; l < 16; l++) {
+      uint32_t b;
+      if (!bits(1, &b)) return -1;
+      code |= (int)b;
+      const int c = H->count[l];
+      if (code - c < first) return H->symbol[index + (code - first)];
+      index += c;
+      first += c;
+      first <<= 1;
+      code <<= 1;
+    }
+    return -1;
+  }
+
+  // ---- output: the history ring, flushed to HBM (bytes below cap) and CRC'd
+  __device__ void flush_to(int64_t upto) {
+    PQG_L uint8_t* ring = lds_ptr(sh->ring);
+    __builtin_amdgcn_wave_barrier();
+    const int64_t nb = upto - flushed;
+    if (nb <= 0) return;
+    // stores: bytes [flushed, upto) below cap, 16-byte granules of the output
+    const int64_t s_hi = upto < cap ? upto : cap;
+    if (s_hi > flushed) {
+      const int64_t g0 = flushed & ~(int64_t)15;
+      for (int64_t g = g0 + 16 * (int64_t)lane; g < s_hi; g += 1024) {
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          uint32_t x = 0;
+#pragma unroll
+          for (int b = 0; b < 4; b++) x |= (uint32_t)ring[(g + 4 * k + b) & (kRing - 1)] << (8 * b);
+          w[k] = x;
+        }
+        if (g >= flushed && g + 16 <= s_hi && ((uintptr_t)(dst + g) & 15) == 0) {
+          stg16((uintptr_t)(dst + g), make_uint4(w[0], w[1], w[2], w[3]));
+        } else {
+          for (int b = 0; b < 16; b++)
+            if (g + b >= flushed && g + b < s_hi) dst[g + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+        }
+      }
+    }
+    // CRC-32 of [flushed, upto): lane slices, combined in a tree
+    const int64_t per = (nb + 63) / 64;
+    const int64_t lo = flushed + per * lane, hi = lo + per < upto ? lo + per : upto;
+    uint32_t c = 0;  // raw (unconditioned) CRC register of the slice
+    for (int64_t i = lo; i < hi; i++) c = lds_ptr(sh->crc_tab)[(c ^ ring[i & (kRing - 1)]) & 0xff] ^ (c >> 8);
+    // combine: crc(A || B) = crc(A) * x^(8 |B|) ^ crc(B) for raw registers
+    int64_t len = hi > lo ? hi - lo : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t oc = (uint32_t)__shfl_down((int)c, o, 64);
+      const int64_t ol = __shfl_down(len, o, 64);
+      if ((lane & (2 * o - 1)) == 0 && lane + o < 64) {
+        c = multmodp(x8nmodp((uint64_t)ol), c) ^ oc;
+        len += ol;
+      }
+    }
+    const uint32_t slice = (uint32_t)__shfl((int)c, 0, 64);
+    // the member's conditioned CRC: crc' = ~( (~crc) * x^(8 nb) ^ raw )
+    crc = ~(multmodp(x8nmodp((uint64_t)nb), ~crc) ^ slice);
+    flushed = upto;
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ __forceinline__ void maybe_flush() {
+    if (d - flushed >= kFlush) flush_to(d);
+  }
+  __device__ __forceinline__ void put(uint32_t byte) {
+    if (lane == 0) lds_ptr(sh->ring)[d & (kRing - 1)] = (uint8_t)byte;
+    d++;
+  }
+  // len bytes from dist back (dist <= bytes of this member so far)
+  __device__ void copy(uint32_t dist, uint32_t len) {
+    PQG_L uint8_t* ring = lds_ptr(sh->ring);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t done = 0;
+    while (done < len) {
+      // a round of min(dist, 64) bytes never reads a byte written in the round
+      const uint32_t step = dist < 64u ? dist : 64u;
+      const uint32_t k = len - done < step ? len - done : step;
+      uint8_t v = 0;
+      if ((uint32_t)lane < k) v = ring[(d + done + lane - dist) & (kRing - 1)];
+      __builtin_amdgcn_wave_barrier();
+      if ((uint32_t)lane < k) ring[(d + done + lane) & (kRing - 1)] = v;
+      __builtin_amdgcn_wave_barrier();
+      done += k;
+    }
+    d += len;
+  }
+
+  // ---- one DEFLATE stream (RFC 1951 3.2.3), kOK or kGZIP
+  __device__ int codes(const Huff& lc, const Huff& dc) {
+    for (;;) {
+      const int sym = decode(lc);
+      if (sym < 0) return kGZIP;
+      if (sym < 256) {
+        put((uint32_t)sym);
+      } else if (sym == 256) {
+        return kOK;
+      } else {
+        const int s = sym - 257;
+        if (s >= 29) return kGZIP;
+        uint32_t e;
+        if (!bits(kLenExt[s], &e)) return kGZIP;
+        const uint32_t len = kLenBase[s] + e;
+        const int ds = decode(dc);
+        if (ds < 0 || ds >= 30) return kGZIP;
+        if (!bits(kDistExt[ds], &e)) return kGZIP;
+        const uint32_t dist = kDistBase[ds] + e;
+        if ((int64_t)dist > d - mstart) return kGZIP;  // "invalid distance too far back"
+        copy(dist, len);
+      }
+      maybe_flush();
+    }
+  }
+  __device__ int stored() {
+    align_byte();
+    uint32_t a, b, c, e;
+    if (!bits(8, &a) || !bits(8, &b) || !bits(8, &c) || !bits(8, &e)) return kGZIP;
+    const uint32_t len = a | b << 8, nlen = c | e << 8;
+    if (len != (~nlen & 0xffffu)) return kGZIP;
+    for (uint32_t k = 0; k < len; k++) {
+      uint32_t v;
+      if (!bits(8, &v)) return kGZIP;
+      put(v);
+      if ((k & 255) == 255) maybe_flush();
+    }
+    maybe_flush();
+    return kOK;
+  }
+  __device__ int fixed() {
+    PQG_L uint16_t* L = lds_ptr(sh->lens);
+    for (int s = lane; s < 288 + 30; s += 64)
+      L[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+    __builtin_amdgcn_wave_barrier();
+    build(sh->lit, sh->lens, 288);
+    build(sh->dist, sh->lens + 288, 30);
+    return codes(sh->lit, sh->dist);
+  }
+  __device__ int dynamic() {
+    uint32_t nlen, ndist, ncode;
+    if (!bits(5, &nlen) || !bits(5, &ndist) || !bits(4, &ncode)) return kGZIP;
+    nlen += 257;
+    ndist += 1;
+    ncode += 4;
+    if (nlen > 286 || ndist > 30) return kGZIP;
+    PQG_L uint16_t* L = lds_ptr(sh->lens);
+    for (int s = lane; s < 19; s += 64) L[s] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t k = 0; k < ncode; k++) {
+      uint32_t v;
+      if (!bits(3, &v)) return kGZIP;
+      if (lane == 0) L[kClOrder[k]] = (uint16_t)v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (build(sh->lit, sh->lens, 19) != 0) return kGZIP;  // the code-length code must be complete
+    // literal/length and distance code lengths (into lens, after the first 19 are used up)
+    uint32_t index = 0;
+    const uint32_t total = nlen + ndist;
+    // decoded lengths go to lens[32 ...] (lens[0..18] hold the code-length code's lengths)
+    PQG_L uint16_t* O = L + 32;
+    while (index < total) {
+      const int sym = decode(sh->lit);
+      if (sym < 0) return kGZIP;
+      if (sym < 16) {
+        if (lane == 0) O[index] = (uint16_t)sym;
+        index++;
+      } else {
+        uint32_t len = 0, rep, e;
+        if (sym == 16) {
+          if (index == 0) return kGZIP;
+          __builtin_amdgcn_wave_barrier();
+          len = O[index - 1];
+          if (!bits(2, &e)) return kGZIP;
+          rep = 3 + e;
+        } else if (sym == 17) {
+          if (!bits(3, &e)) return kGZIP;
+          rep = 3 + e;
+        } else {
+          if (!bits(7, &e)) return kGZIP;
+          rep = 11 + e;
+        }
+        if (index + rep > total) return kGZIP;
+        for (uint32_t k = lane; k < rep; k += 64) O[index + k] = (uint16_t)len;
+        index += rep;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (O[256] == 0) return kGZIP;  // no end-of-block code
+    // move the lengths down: lit/len at lens[0..nlen), distance at lens[288..)
+    uint16_t v[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const uint32_t s = (uint32_t)lane + 64u * k;
+      v[k] = s < total ? O[s] : (uint16_t)0;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const uint32_t s = (uint32_t)lane + 64u * k;
+      if (s < nlen) L[s] = v[k];
+      else if (s < total) L[288 + (s - nlen)] = v[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    // incomplete codes only when all codes have length <= 1 (one code of
+    // length 1: puff, zlib's inflate_table)
+    const int el = build(sh->lit, sh->lens, (int)nlen);
+    if (el < 0 || (el > 0 && (int)nlen != (int)lds_ptr(sh->lit.count)[0] + (int)lds_ptr(sh->lit.count)[1])) return kGZIP;
+    const int ed = build(sh->dist, sh->lens + 288, (int)ndist);
+    if (ed < 0 || (ed > 0 && (int)ndist != (int)lds_ptr(sh->dist.count)[0] + (int)lds_ptr(sh->dist.count)[1]))
+      return kGZIP;
+    return codes(sh->lit, sh->dist);
+  }
+  __device__ int deflate() {
+    uint32_t last, type;
+    do {
+      if (!bits(1, &last) || !bits(2, &type)) return kGZIP;
+      int e;
+      if (type == 0) e = stored();
+      else if (type == 1) e = fixed();
+      else if (type == 2) e = dynamic();
+      else e = kGZIP;
+      if (e) return e;
+    } while (!last);
+    return kOK;
+  }
+
+  // ---- RFC 1952 members until the block ends (Go's multistream reader)
+  __device__ int run() {
+    PQG_L uint32_t* T = lds_ptr(sh->crc_tab);
+    for (int i = lane; i < 256; i += 64) {
+      uint32_t c = (uint32_t)i;
+#pragma unroll
+      for (int k = 0; k < 8; k++) c = c & 1 ? (c >> 1) ^ kCrcPoly : c >> 1;
+      T[i] = c;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (n <= 0) return kGZIP;  // NewReader: io.EOF on an empty block
+    while (pos < n || bitcnt >= 8) {
+      // the header: ID1 ID2 CM FLG MTIME(4) XFL OS, then the optional fields
+      uint32_t hcrc = 0xffffffffu;
+      auto hbyte = [&](uint32_t* v) -> bool {
+        if (!bits(8, v)) return false;
+        hcrc = T[(hcrc ^ *v) & 0xff] ^ (hcrc >> 8);
+        return true;
+      };
+      uint32_t b[10];
+      for (int k = 0; k < 10; k++)
+        if (!hbyte(&b[k])) return kGZIP;
+      if (b[0] != 0x1f || b[1] != 0x8b || b[2] != 8 || (b[3] & 0xe0)) return kGZIP;
+      const uint32_t flg = b[3];
+      uint32_t v, w;
+      if (flg & 4) {  // FEXTRA
+        if (!hbyte(&v) || !hbyte(&w)) return kGZIP;
+        for (uint32_t k = 0; k < (v | w << 8); k++)
+          if (!hbyte(&v)) return kGZIP;
+      }
+      if (flg & 8) {  // FNAME
+        do {
+          if (!hbyte(&v)) return kGZIP;
+        } while (v != 0);
+      }
+      if (flg & 16) {  // FCOMMENT
+        do {
+          if (!hbyte(&v)) return kGZIP;
+        } while (v != 0);
+      }
+      if (flg & 2) {  // FHCRC: the low 16 bits of the header's CRC-32
+        const uint32_t want = ~hcrc & 0xffff;
+        if (!bits(8, &v) || !bits(8, &w)) return kGZIP;
+        if ((v | w << 8) != want) return kGZIP;
+      }
+      mstart = d;
+      crc = 0;
+      int e = deflate();
+      if (e) return e;
+      flush_to(d);
+      // the trailer: CRC-32 and ISIZE (little endian) at the next byte boundary
+      align_byte();
+      uint32_t t[8];
+      for (int k = 0; k < 8; k++)
+        if (!bits(8, &t[k])) return kGZIP;
+      const uint32_t c32 = t[0] | t[1] << 8 | t[2] << 16 | t[3] << 24;
+      const uint32_t isz = t[4] | t[5] << 8 | t[6] << 16 | t[7] << 24;
+      if (c32 != crc || isz != (uint32_t)(d - mstart)) return kGZIP;
+    }
+    return kOK;
+  }
+};
+
+// The serial snappy path's twin for GZIP pages: one wave per page, decoded
+// into the page's scratch block (its uncompressed size, 16-rounded).
+__device__ __forceinline__ void gzip_loc(const PageDev& pg, int64_t* src_off, int64_t* clen, int64_t* ulen) {
+  // V2 pages keep their level bytes raw in front of the compressed values
+  // (page_v2.go:110-123)
+  int64_t lv = 0;
+  if (pg.page_type == 3) lv = (int64_t)(uint32_t)pg.rep_len + (int64_t)(uint32_t)pg.def_len;
+  *src_off = pg.payload_offset + lv;
+  *clen = (int64_t)pg.csize - lv;
+  *ulen = (int64_t)pg.usize - lv;
+}
+
+__global__ void __launch_bounds__(64) k_inflate(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+                                                int* queue, uint8_t* scratch) {
+  __shared__ __attribute__((aligned(16))) InflateShared sh;
+  const int lane = lane_id();
+  for (;;) {
+    const int t = queue_next(queue);
+    if (t >= *total) return;
+    const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
+    const PageDev pg = pages[pidx];
+    if (pg.read_status != kOK || pg.scratch_offset < 0) continue;
+    const JobDev job = jobs[pg.job];
+    if (job.codec != kCodecGzip) continue;
+    int64_t so, clen, ulen;
+    gzip_loc(pg, &so, &clen, &ulen);
+    Inflater f;
+    f.sh = &sh;
+    f.src = gconst(job.data) + so;
+    f.n = clen;
+    f.dst = gmut(scratch) + job.scratch_base + pg.scratch_offset;
+    f.cap = ulen;
+    f.lane = lane;
+    int e = f.run();
+    if (pg.flags & kPageBareBlock) {  // pqg_block_decompress: the decoded length, no size check
+      if (lane == 0) pages[pidx].gz_len = f.d;
+    } else if (e == kOK && f.d != ulen) {
+      e = kSIZE;  // "decompressed data must be %d byte" (compress.go:117)
+    }
+    // V1: getValuesDecoder runs after the block is decompressed (page_v1.go:91-97)
+    if (e == kOK && pg.page_type == 0 && !values_supported(job.type, job.type_length, pg.encoding)) e = kUNSUPPORTED;
+    if (lane == 0 && e != kOK) pages[pidx].read_status = e;
+  }
+}
+
+}  // namespace pqg

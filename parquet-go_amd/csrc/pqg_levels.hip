@@ -73,68 +73,73 @@ __device__ __forceinline__ int reg_stream(const JobDev& job, const PageDev& pg, 
 // one lane per stream: small blocks spread the (latency-bound) lanes over
 // every CU instead of one 256-lane block on each of the first few
 
-struct LaneRing {
-  gcu8 base;       // 16-byte aligned address at or below the stream start
-  uint32_t n;      // stream bytes
-  uint32_t d0;     // stream byte 0 is byte d0 of chunk 0
-  uint32_t cur;    // chunk of the current position (slots hold cur, cur+1)
-  PQG_L uint32_t* lds;  // dword k of slot s at lds[(16 s + k) * kWalkThreads]
-
-  // Load chunk c into its slot.  No prefetch is carried in registers across
-  // iterations: a loop-carried register holding an in-flight load makes the
-  // compiler wait for it (vmcnt(0)) at every iteration's latch, and that wait
-  // also covers the run-table store just issued.
-  __device__ __forceinline__ void load(uint32_t c) {
-    uint4 r[4];
+constexpr int kLaneWinG = 8;  // 16-byte granules of a lane's window (128 bytes)
+struct LaneWin {
+  gcu8 p;
+  uint32_t n;
+  uint32_t base;           // stream offset of window byte 0 (16-aligned address; may precede the stream: wraps)
+  PQG_L uint32_t* r;       // dword k of the window at r[64 k]
+  // The window at the granule holding stream byte pos.  Every load is issued
+  // unconditionally before the first is used (a granule past the stream
+  // re-reads its last one, mapped): the loads of a lane then cost one wait —
+  // which also waits for the lane's earlier level stores, vmcnt retiring in
+  // order — instead of one per guarded load.
+  __device__ __forceinline__ void fill(uint32_t pos) {
+    const uint32_t mis = (uint32_t)((uintptr_t)(p + pos) & 15);
+    base = pos - mis;
+    const uintptr_t a0 = (uintptr_t)(p + pos) - mis;
+    const uintptr_t last = ((uintptr_t)(p + n) - 1) & ~(uintptr_t)15;  // n > pos >= 0
+    uint4 g[kLaneWinG];
 #pragma unroll
-    for (int g = 0; g < 4; g++) {
-      // granule [c*64 + 16g - d0, +16): mapped when it holds a stream byte < n
-      const int64_t s0 = (int64_t)c * 64 + 16 * g - d0;
-      r[g] = (s0 < (int64_t)n && s0 + 16 > 0) ? ldg16((uintptr_t)(base + (size_t)c * 64 + 16 * g))
-                                               : make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < kLaneWinG; k++) {
+      const uintptr_t a = a0 + 16 * k;
+      g[k] = ldg16(a <= last ? a : last);
     }
-    PQG_L uint32_t* b = lds + (c & 1) * 16 * kWalkThreads;
 #pragma unroll
-    for (int g = 0; g < 4; g++) {
-      b[(4 * g + 0) * kWalkThreads] = r[g].x;
-      b[(4 * g + 1) * kWalkThreads] = r[g].y;
-      b[(4 * g + 2) * kWalkThreads] = r[g].z;
-      b[(4 * g + 3) * kWalkThreads] = r[g].w;
+    for (int k = 0; k < kLaneWinG; k++) {
+      const uint4 v = mask_tail(g[k], (int64_t)pos - mis + 16 * k, n);  // bytes past n read as zero (Q5)
+      r[64 * (4 * k + 0)] = v.x;
+      r[64 * (4 * k + 1)] = v.y;
+      r[64 * (4 * k + 2)] = v.z;
+      r[64 * (4 * k + 3)] = v.w;
     }
   }
-  __device__ __forceinline__ void move_to(uint32_t c) {
-    if (c != cur + 1) load(c);  // a jump: both chunks are new
-    load(c + 1);
-    cur = c;
+  __device__ __forceinline__ void ensure(uint32_t pos) {
+    if (pos - base > 16 * kLaneWinG - 16) fill(pos);
   }
-  __device__ __forceinline__ void init(const uint8_t* p, uint32_t n_, PQG_L uint32_t* lds_) {
-    d0 = (uint32_t)((uintptr_t)p & 15);
-    base = gconst(p) - d0;
-    n = n_;
-    lds = lds_;
-    cur = 0xfffffff0u;
-    move_to(0);
+  // 12 bytes at stream offset pos (window already holding [pos, pos + 16))
+  __device__ __forceinline__ void read12(uint32_t pos, uint32_t& a, uint32_t& b, uint32_t& c) const {
+    const uint32_t off = pos - base;
+    const uint32_t d = off >> 2, sh = (off & 3) * 8;
+    const uint32_t x0 = r[64 * d], x1 = r[64 * (d + 1)], x2 = r[64 * (d + 2)], x3 = r[64 * (d + 3)];
+    a = __builtin_amdgcn_alignbit(x1, x0, sh);
+    b = __builtin_amdgcn_alignbit(x2, x1, sh);
+    c = __builtin_amdgcn_alignbit(x3, x2, sh);
   }
-  // 8 bytes at stream position pos (< n; bytes past n are garbage)
-  __device__ __forceinline__ uint64_t peek8(uint32_t pos) {
-    const uint32_t off = pos + d0;
-    const uint32_t c = off >> 6;
-    if (c != cur) move_to(c);
-    const uint32_t k0 = ((c & 1) << 4) | ((off >> 2) & 15);
-    const uint32_t a = lds[k0 * kWalkThreads], b = lds[((k0 + 1) & 31) * kWalkThreads],
-                   cc = lds[((k0 + 2) & 31) * kWalkThreads];
-    const uint32_t sh = (off & 3) * 8;
-    const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sh), hi = __builtin_amdgcn_alignbit(cc, b, sh);
-    return (uint64_t)lo | (uint64_t)hi << 32;
+  __device__ __forceinline__ void peek12(uint32_t pos, uint32_t& a, uint32_t& b, uint32_t& c) {
+    ensure(pos);
+    read12(pos, a, b, c);
   }
 };
+
+// The lanes of a wave refill their windows together: a lane whose next read
+// leaves its window votes, and then every lane that reads this step refills
+// at its read position.  Each refill waits for the wave's earlier stores
+// (vmcnt retires in order), so per-lane refills at scattered steps would stall
+// the wave on memory almost every step; together they cost one stall per
+// window's worth of progress of the fastest lane.
+__device__ __forceinline__ void sync_ensure(LaneWin& w, bool reads, uint32_t rp) {
+  const bool need = reads && rp - w.base > 16 * kLaneWinG - 16;
+  if (__ballot(need) != 0 && reads) w.fill(rp);
+}
 
 // Lanes [0, total) walk the rep streams, [total, 2 total) the def streams,
 // [2 total, 3 total) the value streams, so a wave's lanes do alike work.
 __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pages, const int* list, const int* total,
                                                               HStream* streams, RunEnt* runs, BlockDesc* blks,
                                                               LongWalk* longs, int long_cap) {
-  __shared__ uint32_t buf[32 * kWalkThreads];  // two 64-byte chunks per lane
+  static_assert(kWalkThreads == 64, "LaneWin: dword k of lane L at buf[64 k + L]");
+  __shared__ uint32_t buf[4 * kLaneWinG * kWalkThreads];  // each lane's 128-byte window (LaneWin)
   const int nt = *total;
   int* const n_long = const_cast<int*>(total) + kCtrLongWalk;
   // level streams are decoded in place by k_page_levels: only the value streams
@@ -150,8 +155,8 @@ __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pag
     const uint64_t vmask = rb >= 4 ? 0xffffffffull : ((1ull << (8 * rb)) - 1);
     PQG_G uint32_t* R = (PQG_G uint32_t*)(gmut(runs) + S.run_base);
     PQG_G uint32_t* B = (PQG_G uint32_t*)(gmut(blks) + S.blk_base);
-    LaneRing rd;
-    rd.init(S.p, n, lds_ptr(buf) + threadIdx.x);
+    LaneWin rd{gconst(S.p), n, 0xfffffff0u, lds_ptr(buf) + threadIdx.x};
+    if (n > 0) rd.fill(0);
     uint32_t pos = 0, produced = 0, nr = 0;
     int status = kOK;
     // block under construction (see BlockDesc)
@@ -168,7 +173,10 @@ __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pag
     while (produced < count) {
       // hybridDecoder.next: run header = readUVariant32 (helpers.go:149-165)
       if (pos >= n) { status = kEOF; break; }
-      uint64_t x = rd.peek8(pos);
+      sync_ensure(rd, true, pos);
+      uint32_t xa, xb, xc;
+      rd.read12(pos, xa, xb, xc);
+      uint64_t x = (uint64_t)xa | (uint64_t)xb << 32;
       uint32_t h, hl;
       if ((x & 0x80) == 0) {
         h = (uint32_t)x & 0x7f;
@@ -180,7 +188,14 @@ __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pag
         hl = 0;
         for (uint32_t i = 0;; i++) {
           if (pos + i >= n) { e = kEOF; break; }
-          const uint32_t b = i < 8 ? (uint32_t)(x >> (8 * i)) & 0xff : (uint32_t)rd.peek8(pos + i) & 0xff;
+          uint32_t b;
+          if (i < 8) {
+            b = (uint32_t)(x >> (8 * i)) & 0xff;
+          } else {
+            uint32_t ya, yb, yc;
+            rd.peek12(pos + i, ya, yb, yc);
+            b = ya & 0xff;
+          }
           if (b < 0x80) {
             if (i > 9 || (i == 9 && b > 1)) e = kRLE;  // overflows uint64
             else {
@@ -195,7 +210,11 @@ __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pag
         }
         if (e) { status = e; break; }
         h = (uint32_t)v;
-        x = rd.peek8(pos + hl) << 8;  // the RLE value at byte 1, like the fast path
+        {
+          uint32_t ya, yb, yc;
+          rd.peek12(pos + hl, ya, yb, yc);
+          x = ((uint64_t)ya | (uint64_t)yb << 32) << 8;  // the RLE value at byte 1, like the fast path
+        }
       }
       pos += hl;
       uint32_t take, st, src;
@@ -1023,9 +1042,109 @@ __device__ __forceinline__ int level_stream(gcu8 p, int64_t n, int w, uint32_t c
   return e;
 }
 
-// Setup (the read phase of the page, as k_page_setup) and the level decode
-// (as k_levels_expand) of one data page per wave; the value streams are
-// registered for the walker.
+// The read phase of one data page (V1 initSize: page_v1.go:99-105,
+// hybrid_decoder.go:57-67; V2 raw level bytes: page_v2.go:103-121): its block,
+// level and value streams, the value stream registered for the walker
+// (dictionary indices type_dict.go:22-37, RLE booleans type_boolean.go:100-120)
+// and its values stage.  `writer`: this thread writes the page record.
+struct PageStreams {
+  gcu8 rep, def;
+  int64_t rep_n, def_n;  // -1: the level decoder is not initialised
+  int e;                 // read-phase error
+};
+__device__ __forceinline__ PageStreams page_setup(const JobDev& job, const PageDev& pg, int pidx, PageDev* pages,
+                                                  HStream* streams, const int* total, const uint8_t* scratch,
+                                                  bool writer) {
+  PageStreams r{nullptr, nullptr, -1, -1, kOK};
+  gcu8 block;
+  int64_t blen;
+  int32_t levels = 0;
+  if (pg.page_type == 3) {
+    levels = (int32_t)((uint32_t)pg.rep_len + (uint32_t)pg.def_len);
+    blen = (int32_t)((uint32_t)pg.csize - (uint32_t)levels);
+    if (pg.scratch_offset >= 0) blen = (int32_t)((uint32_t)pg.usize - (uint32_t)levels);
+  } else {
+    blen = pg.scratch_offset >= 0 ? pg.usize : pg.csize;
+  }
+  if (pg.scratch_offset >= 0) block = gconst(scratch) + job.scratch_base + pg.scratch_offset;
+  else block = gconst(job.data) + pg.payload_offset + (levels > 0 ? levels : 0);
+  int64_t vpos = 0;
+  if (pg.page_type == 0) {
+    // rDecoder.initSize then dDecoder.initSize (page_v1.go:99-105)
+    if (job.max_rep > 0) {
+      if (blen - vpos < 4) r.e = kEOF;
+      else {
+        const int64_t sz = rd_u32(block + vpos);
+        const int64_t take = min(sz, blen - vpos - 4);
+        r.rep = block + vpos + 4;
+        r.rep_n = take;
+        vpos += 4 + take;
+      }
+    }
+    if (r.e == kOK && job.max_def > 0) {
+      if (blen - vpos < 4) r.e = kEOF;
+      else {
+        const int64_t sz = rd_u32(block + vpos);
+        const int64_t take = min(sz, blen - vpos - 4);
+        r.def = block + vpos + 4;
+        r.def_n = take;
+        vpos += 4 + take;
+      }
+    }
+  } else {
+    // V2: raw level bytes, a decoder only for a non-empty section (page_v2.go:110-120)
+    gcu8 lv = gconst(job.data) + pg.payload_offset;
+    if (levels > 0 && pg.rep_len > 0) { r.rep = lv; r.rep_n = pg.rep_len; }
+    if (levels > 0 && pg.def_len > 0) { r.def = lv + pg.rep_len; r.def_n = levels - pg.rep_len; }
+  }
+  if (r.e != kOK) {
+    if (writer) pages[pidx].read_status = r.e;
+    return r;
+  }
+  const int64_t n = pg.num_values;
+  const int64_t vn = blen - vpos;
+  gcu8 val = block + vpos;
+  if (writer) {
+    PageDev& P = pages[pidx];
+    P.block = (const uint8_t*)block;
+    P.block_len = blen;
+    P.val = (const uint8_t*)val;
+    P.val_n = vn;
+    P.rep = (const uint8_t*)r.rep;
+    P.rep_n = r.rep_n;
+    P.def = (const uint8_t*)r.def;
+    P.def_n = r.def_n;
+    // values: RLE_DICTIONARY indices (first byte = bit width) / RLE booleans (u32 length)
+    if (pg.encoding == 8 && vn >= 1) {
+      const int wv = val[0];
+      P.dict_width = wv;
+      if (wv >= 1 && wv <= 32 && n > 0) reg_stream(job, pg, streams, &P.hs_val, pidx, 2, val + 1, vn - 1, wv, n);
+    } else if (pg.encoding == 3 && job.type == 0 && vn >= 4) {
+      const int64_t sz = rd_u32(val);
+      const int64_t take = min(sz, vn - 4);
+      if (n > 0) reg_stream(job, pg, streams, &P.hs_val, pidx, 3, val + 4, take, 1, n);
+    }
+    // value-stage page lists: 4-byte dictionary pages (the hot path, a kernel
+    // of its own), variable-length values (pqg_strings.hip) and everything else
+    // (DELTA_BYTE_ARRAY on FLBA: the strings stage, values of type_length bytes)
+    const int vm = job.value_width == 0 || (pg.encoding == 7 && job.type == 7) ? 2
+                   : (pg.encoding == 8 && job.value_width == 4)                ? 1
+                   : pg.encoding == 5                                          ? 3
+                                                                               : 0;
+    P.vmode = vm;
+    int* present = const_cast<int*>(total) + kModePresentOff;
+    if (present[vm] == 0) present[vm] = 1;
+    // flag 4: DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY pages (k_str_delta, k_str_dba)
+    if (vm == 2 && (pg.encoding == 6 || pg.encoding == 7) && present[4] == 0) present[4] = 1;
+  }
+  return r;
+}
+
+// Setup and the level decode of one data page per wave (the speculative
+// window parse above).  (A lane-per-page walk of the level streams was tried
+// and dropped: with one lane per page a 35 000-page batch fills ~550 waves,
+// and each lane's serial walk of ~1 100 runs and 1 250 granules ran 4x slower
+// than this kernel: DESIGN.md.)
 __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total,
                                                     int* queue, uint8_t* scratch, HStream* streams,
                                                     uint8_t* def_arena, uint8_t* rep_arena, LongLev* longs,
@@ -1045,109 +1164,27 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
     if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3)) continue;
     const JobDev job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
-    // ---- the page block and its level / value streams (read phase)
-    gcu8 block;
-    int64_t blen;
-    int32_t levels = 0;
-    if (pg.page_type == 3) {
-      levels = (int32_t)((uint32_t)pg.rep_len + (uint32_t)pg.def_len);
-      blen = (int32_t)((uint32_t)pg.csize - (uint32_t)levels);
-      if (pg.scratch_offset >= 0) blen = (int32_t)((uint32_t)pg.usize - (uint32_t)levels);
-    } else {
-      blen = pg.scratch_offset >= 0 ? pg.usize : pg.csize;
-    }
-    if (pg.scratch_offset >= 0) block = gconst(scratch) + job.scratch_base + pg.scratch_offset;
-    else block = gconst(job.data) + pg.payload_offset + (levels > 0 ? levels : 0);
-    gcu8 rep = nullptr, def = nullptr;
-    int64_t rep_n = -1, def_n = -1;  // -1: the level decoder is not initialised
-    int64_t vpos = 0;
-    int e = kOK;
-    if (pg.page_type == 0) {
-      // rDecoder.initSize then dDecoder.initSize (page_v1.go:99-105)
-      if (job.max_rep > 0) {
-        if (blen - vpos < 4) e = kEOF;
-        else {
-          const int64_t sz = rd_u32(block + vpos);
-          const int64_t take = min(sz, blen - vpos - 4);
-          rep = block + vpos + 4;
-          rep_n = take;
-          vpos += 4 + take;
-        }
-      }
-      if (e == kOK && job.max_def > 0) {
-        if (blen - vpos < 4) e = kEOF;
-        else {
-          const int64_t sz = rd_u32(block + vpos);
-          const int64_t take = min(sz, blen - vpos - 4);
-          def = block + vpos + 4;
-          def_n = take;
-          vpos += 4 + take;
-        }
-      }
-    } else {
-      // V2: raw level bytes, a decoder only for a non-empty section (page_v2.go:110-120)
-      gcu8 lv = gconst(job.data) + pg.payload_offset;
-      if (levels > 0 && pg.rep_len > 0) { rep = lv; rep_n = pg.rep_len; }
-      if (levels > 0 && pg.def_len > 0) { def = lv + pg.rep_len; def_n = levels - pg.rep_len; }
-    }
-    if (e != kOK) {
-      if (lane == 0) pages[pidx].read_status = e;
-      continue;
-    }
+    const PageStreams ps = page_setup(job, pg, pidx, pages, streams, total, scratch, lane == 0);
+    if (ps.e != kOK) continue;
     const int64_t n = pg.num_values;
-    const int64_t vn = blen - vpos;
-    gcu8 val = block + vpos;
-    if (lane == 0) {
-      PageDev& P = pages[pidx];
-      P.block = (const uint8_t*)block;
-      P.block_len = blen;
-      P.val = (const uint8_t*)val;
-      P.val_n = vn;
-      P.rep = (const uint8_t*)rep;
-      P.rep_n = rep_n;
-      P.def = (const uint8_t*)def;
-      P.def_n = def_n;
-      // values: RLE_DICTIONARY indices (first byte = bit width) / RLE booleans (u32 length)
-      if (pg.encoding == 8 && vn >= 1) {
-        const int wv = val[0];
-        P.dict_width = wv;
-        if (wv >= 1 && wv <= 32 && n > 0) reg_stream(job, pg, streams, &P.hs_val, pidx, 2, val + 1, vn - 1, wv, n);
-      } else if (pg.encoding == 3 && job.type == 0 && vn >= 4) {
-        const int64_t sz = rd_u32(val);
-        const int64_t take = min(sz, vn - 4);
-        if (n > 0) reg_stream(job, pg, streams, &P.hs_val, pidx, 3, val + 4, take, 1, n);
-      }
-      // value-stage page lists: 4-byte dictionary pages (the hot path, a kernel
-      // of its own), variable-length values (pqg_strings.hip) and everything else
-      // (DELTA_BYTE_ARRAY on FLBA: the strings stage, values of type_length bytes)
-      const int vm = job.value_width == 0 || (pg.encoding == 7 && job.type == 7) ? 2
-                     : (pg.encoding == 8 && job.value_width == 4)                ? 1
-                     : pg.encoding == 5                                          ? 3
-                                                                                 : 0;
-      P.vmode = vm;
-      int* present = const_cast<int*>(total) + kModePresentOff;
-      if (present[vm] == 0) present[vm] = 1;
-      // flag 4: DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY pages (k_str_delta, k_str_dba)
-      if (vm == 2 && (pg.encoding == 6 || pg.encoding == 7) && present[4] == 0) present[4] = 1;
-    }
     // ---- readValues (page_v1.go:27-55): rep levels, then def levels
     int64_t nn = 0;
     int de = kOK;
     if (n > 0) {
       if (job.max_rep > 0) {
-        if (rep_n < 0) de = kLEVELS;  // V2 with no rep-level bytes: "reader is not initialized"
+        if (ps.rep_n < 0) de = kLEVELS;  // V2 with no rep-level bytes: "reader is not initialized"
         else {
           uint32_t unused;
-          de = level_stream(rep, rep_n, bits_len((uint32_t)job.max_rep), (uint32_t)n,
+          de = level_stream(ps.rep, ps.rep_n, bits_len((uint32_t)job.max_rep), (uint32_t)n,
                             gmut(rep_arena) + job.slot_base + pg.slot_offset, 0x100u, sh, &unused, lt, pidx);
         }
       }
       if (de == kOK) {
         if (job.max_def > 0) {
-          if (def_n < 0) de = kLEVELS;
+          if (ps.def_n < 0) de = kLEVELS;
           else {
             uint32_t c;
-            de = level_stream(def, def_n, bits_len((uint32_t)job.max_def), (uint32_t)n,
+            de = level_stream(ps.def, ps.def_n, bits_len((uint32_t)job.max_def), (uint32_t)n,
                               gmut(def_arena) + job.slot_base + pg.slot_offset, (uint32_t)job.max_def, sh, &c, lt,
                               pidx);
             nn = c;

@@ -44,6 +44,8 @@ __global__ void k_page_list(JobDev* jobs, PageDev* pages, int n_jobs, int* list,
                             int* queues);
 __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                          uint8_t* scratch);
+__global__ void k_inflate(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                          uint8_t* scratch);
 __global__ void k_snap_plan(const JobDev* jobs, PageDev* pages, const int* list, const int* total, int* ctr,
                             SnapSub* subs, int sub_cap, int* seg_page, int seg_cap);
 __global__ void k_snap_seg(const JobDev* jobs, const PageDev* pages, const int* seg_page, const int* seg_total,
@@ -523,13 +525,19 @@ static int launch_pipeline(pqg_ctx* c) {
   hipLaunchKernelGGL(k_page_list, dim3(n), dim3(1024), 0, s, jobs, pages, n, list,
                      (int)std::min<int64_t>(c->list_cap, INT32_MAX), ctr, ctr + 8);
   if (c->timed) hipEventRecord(c->ev[2], s);
-  bool any_comp = false;
-  for (int i = 0; i < n; i++) any_comp |= c->cur[(size_t)i].col.codec != PQG_CODEC_UNCOMPRESSED;
-  if (any_comp) {
+  bool any_snappy = false, any_gzip = false;
+  for (int i = 0; i < n; i++) {
+    any_snappy |= c->cur[(size_t)i].col.codec == PQG_CODEC_SNAPPY;
+    any_gzip |= c->cur[(size_t)i].col.codec == PQG_CODEC_GZIP;
+  }
+  if (any_snappy) {
     const SnapTables T{(SnapSub*)c->sn_subs.p, (int)std::min<int64_t>(c->sn_sub_cap, INT32_MAX), (int*)c->sn_segpage.p,
                        (int)std::min<int64_t>(c->sn_seg_cap, INT32_MAX), (uint2*)c->sn_F.p};
     launch_snappy(c, s, jobs, pages, list, ctr, c->list_cap, ctr + 32, Q(0), Q(kQueueSnapSerial), scratch, T);
   }
+  if (any_gzip)  // one wave per GZIP page (pqg_inflate.hip)
+    hipLaunchKernelGGL(k_inflate, dim3(qgrid(c->num_cus * 4)), dim3(64), 0, s, jobs, pages, list, ctr, Q(kQueueInflate),
+                       scratch);
   if (c->timed) hipEventRecord(c->ev[3], s);
   HStream* streams = (HStream*)c->streams.p;
   RunEnt* runs = (RunEnt*)c->runs.p;
@@ -781,6 +789,56 @@ int pqg_decode_page(pqg_ctx* c, const pqg_page_job* pj, pqg_chunk_result* result
   return pqg_decode_chunks(c, &job, 1, result);
 }
 
+// gzipCompressor.DecompressBlock (compress.go:63-76): gzip.NewReader +
+// ioutil.ReadAll.  The decoded length is not in the block, so k_inflate decodes
+// it as a bare block (kPageBareBlock): bytes past `cap` are counted and CRC'd
+// but not stored, and the count comes back in PageDev.gz_len.
+static int block_inflate(pqg_ctx* c, const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int64_t* out_len) {
+  const int64_t store = std::min<int64_t>(std::max<int64_t>(cap, 0), INT32_MAX);
+  hipSetDevice(c->device);
+  if (c->blk_src.grow((size_t)n + 64) || c->blk_dst.grow((size_t)store + 64) ||
+      c->blk_meta.grow(sizeof(JobDev) + sizeof(PageDev) + (4 + 2 * kQueueInts) * sizeof(int)))
+    return PQG_ERR_HIP;
+  JobDev jd;
+  memset(&jd, 0, sizeof(jd));
+  jd.data = (const uint8_t*)c->blk_src.p;
+  jd.data_len = n;
+  jd.tcs = n;
+  jd.codec = PQG_CODEC_GZIP;
+  jd.scratch_cap = store + 16;
+  PageDev pd;
+  memset(&pd, 0, sizeof(pd));
+  pd.page_type = PQG_PAGE_DICTIONARY;  // no values-decoder check after the block
+  pd.flags = kPageBareBlock;
+  pd.csize = (int32_t)n;
+  pd.usize = (int32_t)store;
+  pd.read_status = kOK;
+  uint8_t* meta = (uint8_t*)c->blk_meta.p;
+  JobDev* djob = (JobDev*)meta;
+  PageDev* dpage = (PageDev*)(meta + sizeof(JobDev));
+  int* ints = (int*)(meta + sizeof(JobDev) + sizeof(PageDev));  // [0] list, [1] total, then the queue
+  int hi[2] = {0, 1};
+  if ((n && hipMemcpyAsync(c->blk_src.p, src, (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess) ||
+      hipMemcpyAsync(djob, &jd, sizeof(jd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(dpage, &pd, sizeof(pd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(ints, hi, sizeof(hi), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemsetAsync(ints + 4, 0, sizeof(int) * kQueueInts, c->stream) != hipSuccess)
+    return PQG_ERR_HIP;
+  hipLaunchKernelGGL(k_inflate, dim3(qgrid(1)), dim3(64), 0, c->stream, djob, dpage, ints, ints + 1, ints + 4,
+                     (uint8_t*)c->blk_dst.p);
+  if (hipGetLastError() != hipSuccess) return PQG_ERR_HIP;
+  if (hipMemcpyAsync(&pd, dpage, sizeof(pd), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return PQG_ERR_HIP;
+  if (pd.read_status != kOK) return pd.read_status;
+  *out_len = pd.gz_len;
+  if (pd.gz_len > cap) return PQG_ERR_CAPACITY;
+  if (pd.gz_len && (hipMemcpyAsync(dst, c->blk_dst.p, (size_t)pd.gz_len, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                    hipStreamSynchronize(c->stream) != hipSuccess))
+    return PQG_ERR_HIP;
+  return PQG_OK;
+}
+
 int pqg_block_decompress(pqg_ctx* c, int codec, const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap,
                          int64_t* out_len) {
   if (!c || (!src && n > 0) || n < 0 || n > INT32_MAX || !out_len) return PQG_ERR_INVALID_ARG;
@@ -791,6 +849,7 @@ int pqg_block_decompress(pqg_ctx* c, int codec, const uint8_t* src, int64_t n, u
     if (n) memcpy(dst, src, (size_t)n);
     return PQG_OK;
   }
+  if (codec == PQG_CODEC_GZIP) return block_inflate(c, src, n, dst, cap, out_len);
   if (codec != PQG_CODEC_SNAPPY) return PQG_ERR_UNSUPPORTED;
   // decodedLen (decode.go:32-43): the varint header, on the host to size the output
   uint64_t v = 0;

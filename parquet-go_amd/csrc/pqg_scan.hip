@@ -70,7 +70,7 @@ __device__ __forceinline__ int classify_page(const JobDev& job, const PageHdr& h
     else if (h.csize < 0 || h.usize < 0) e = kPAGE_HEADER;
     else if (job.data_len - payload < (int64_t)h.csize) e = kSIZE;
     else if (job.codec == 0) { if (h.csize != h.usize) e = kSIZE; }
-    else if (job.codec == 1) *comp = ((int64_t)h.usize + 15) & ~(int64_t)15;
+    else if (job.codec == kCodecSnappy || job.codec == kCodecGzip) *comp = ((int64_t)h.usize + 15) & ~(int64_t)15;
     else e = kUNSUPPORTED;
     *next = payload + h.csize;
     if (e == kOK && job.has_dict_off) *next = job.data_page_offset;
@@ -86,9 +86,9 @@ __device__ __forceinline__ int classify_page(const JobDev& job, const PageHdr& h
     else if (h.csize < 0 || h.usize < 0) e = kPAGE_HEADER;
     else if (job.data_len - payload < (int64_t)h.csize) e = kSIZE;
     else if (job.codec == 0 && h.csize != h.usize) e = kSIZE;
-    else if (job.codec != 0 && job.codec != 1) e = kUNSUPPORTED;
+    else if (job.codec != 0 && job.codec != kCodecSnappy && job.codec != kCodecGzip) e = kUNSUPPORTED;
     else if (job.codec == 0 && !values_supported(job.type, job.type_length, enc)) e = kUNSUPPORTED;
-    if (e == kOK && job.codec == 1) *comp = ((int64_t)h.usize + 15) & ~(int64_t)15;
+    if (e == kOK && job.codec != 0) *comp = ((int64_t)h.usize + 15) & ~(int64_t)15;
     *next = payload + h.csize;
   } else if (h.type == 3) {  // DATA_PAGE_V2 (page_v2.go:56-129)
     pg.num_values = h.has_v2 ? h.num_values : 0;
@@ -105,8 +105,8 @@ __device__ __forceinline__ int classify_page(const JobDev& job, const PageHdr& h
     else if (cs < 0 || us < 0) e = kPAGE_HEADER;
     else if (job.data_len - body < (int64_t)cs) e = kSIZE;
     else if (job.codec == 0 && cs != us) e = kSIZE;
-    else if (job.codec != 0 && job.codec != 1) e = kUNSUPPORTED;
-    if (e == kOK && job.codec == 1) *comp = ((int64_t)us + 15) & ~(int64_t)15;
+    else if (job.codec != 0 && job.codec != kCodecSnappy && job.codec != kCodecGzip) e = kUNSUPPORTED;
+    if (e == kOK && job.codec != 0) *comp = ((int64_t)us + 15) & ~(int64_t)15;
     *next = body + cs;
   } else {
     e = kUNSUPPORTED;  // "DATA_PAGE or DATA_PAGE_V2 type supported"

@@ -877,7 +877,9 @@ __global__ void __launch_bounds__(256) k_snap_plan(const JobDev* jobs, PageDev* 
     if (t < n) {
       pidx = list[t];
       PageDev& pg = pages[pidx];
-      if (pg.read_status == kOK && pg.scratch_offset >= 0) {
+      // snappy pages only (GZIP pages: k_inflate); every other page leaves here
+      // with an empty split (nsub = nseg = 0, no fallback)
+      if (pg.read_status == kOK && pg.scratch_offset >= 0 && jobs[pg.job].codec == kCodecSnappy) {
         const JobDev& job = jobs[pg.job];
         const SnapLoc L = snap_loc(pg);
         const PQG_G uint8_t* src = gconst(job.data) + L.src_off;
@@ -1101,6 +1103,7 @@ __global__ void __launch_bounds__(64) k_snappy(JobDev* jobs, PageDev* pages, con
     if (pg.read_status != kOK || pg.scratch_offset < 0 || !pg.sn_fallback) continue;
     const SnapLoc L = snap_loc(pg);
     const JobDev job = jobs[pg.job];
+    if (job.codec != kCodecSnappy) continue;
     SnapBlock blk{gconst(job.data) + L.src_off, L.clen, gmut(scratch) + job.scratch_base + pg.scratch_offset, L.ulen,
                   &sh};
     int hl = 0;
