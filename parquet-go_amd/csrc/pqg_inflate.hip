@@ -469,7 +469,8 @@ struct Inflater {
       uint32_t v, w;
       if (flg & 4) {  // FEXTRA
         if (!hbyte(&v) || !hbyte(&w)) return kGZIP;
-        for (uint32_t k = 0; k < (v | w << 8); k++)
+        const uint32_t xlen = v | w << 8;
+        for (uint32_t k = 0; k < xlen; k++)
           if (!hbyte(&v)) return kGZIP;
       }
       if (flg & 8) {  // FNAME

@@ -1203,8 +1203,14 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
 
 // ---- K3d ---------------------------------------------------------------------
 // notNull prefix per chunk + dictionary-page resolution; one 256-lane block per job.
-__global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch) {
+__device__ void plan_parts(JobDev& job, int np, bool fail, const PageDev* pp, const HStream* streams,
+                           const BlockDesc* blks, int* ctr, PartRec* parts, int64_t cap, int64_t* part);
+
+__global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch,
+                                                  const HStream* streams, const BlockDesc* blks, int* ctr,
+                                                  PartRec* parts, int64_t parts_cap) {
   __shared__ int64_t part[17];
+  __shared__ int s_cap;
   JobDev& job = jobs[blockIdx.x];
   int np = job.num_pages < job.page_cap ? job.num_pages : job.page_cap;
   if (job.status == kCAPACITY) np = 0;
@@ -1228,10 +1234,12 @@ __global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, 
     pp[i].value_offset = run;
     run += nn_of(i);
   }
+  const bool fail0 = job.status == kCAPACITY;
   if (threadIdx.x == 0) {
+    s_cap = fail0;
     job.num_values = carry;
     const int64_t vb = job.value_width > 0 ? carry * job.value_width : 0;
-    if (job.value_width > 0 && vb > job.value_cap) job.status = kCAPACITY;
+    if (job.value_width > 0 && vb > job.value_cap) job.status = kCAPACITY, s_cap = 1;
     job.values_bytes = vb;
     // dictionary page (page_dict.go:30-64): PLAIN entries of the column type.
     // The dictionary is published only when the page's read phase succeeds:
@@ -1262,7 +1270,7 @@ __global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, 
           // (every entry takes >= 4 bytes: a walk fails before entry blen/4 + 1)
           flags = 2;
           job.need_doffs = (cnt < blen / 4 ? cnt : blen / 4) + 2;
-          if (job.need_doffs > job.doffs_cap) job.status = kCAPACITY;
+          if (job.need_doffs > job.doffs_cap) job.status = kCAPACITY, s_cap = 1;
         }
         if (st == kOK) {
           job.flags |= flags;
@@ -1275,6 +1283,9 @@ __global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, 
       }
     }
   }
+  __syncthreads();
+  // values-stage parts (below)
+  plan_parts(job, np, s_cap != 0, pp, streams, blks, ctr, parts, parts_cap, part);
 }
 
 }  // namespace pqg
@@ -1282,7 +1293,7 @@ __global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, 
 namespace pqg {
 
 // ---- values-stage parts -----------------------------------------------------
-// Per job (one 1024-thread block, after k_nn_scan): every set-up data page
+// Per job (the tail of k_nn_scan's 1024-thread block): every set-up data page
 // gets one PartRec, a page of more than kSplitMin values (parquet-go's writer:
 // the whole chunk) several (see pqg_common.h); the job's parts are contiguous,
 // in page order, from a slot range taken with one atomic.
@@ -1293,7 +1304,7 @@ __device__ __forceinline__ int64_t part_count(const PageDev& pg, const HStream* 
   const int enc = pg.encoding;
   if (pg.vmode == 2 && enc != 0 && enc != 8) return 0;  // DELTA_(LENGTH_)BYTE_ARRAY: one part
   const int64_t nn = pg.not_null;
-  if (enc == 0) return nn;                                // PLAIN: value ranges
+  if (enc == 0 || nn <= kSplitMin) return nn;            // PLAIN: value ranges; small pages: one part
   if ((enc == 8 || enc == 3) && pg.hs_val >= 0) {         // hybrid value stream: block ranges
     const HStream& S = streams[pg.hs_val];
     *hyb = true;
@@ -1302,86 +1313,85 @@ __device__ __forceinline__ int64_t part_count(const PageDev& pg, const HStream* 
   return 0;
 }
 
-__global__ void __launch_bounds__(1024) k_part_plan(JobDev* jobs, const PageDev* pages, const HStream* streams,
-                                                    const BlockDesc* blks, int* ctr, PartRec* parts, int64_t cap) {
-  __shared__ int64_t part[17];
+__device__ __forceinline__ int64_t part_n(const PageDev& pg, const HStream* streams, int64_t* count, bool* hyb) {
+  const int64_t c = part_count(pg, streams, hyb);
+  *count = c;
+  if (c < 0) return 0;
+  return c > kSplitMin ? (c + kPart - 1) / kPart : 1;
+}
+
+// Called by k_nn_scan's block after its scan (the job's status in `fail`).
+// Each thread takes a contiguous segment of pages (independent loads, as in
+// the nn scan); one block scan gives every page its first slot.  Single-part
+// pages are written by their thread; split pages go through an LDS list, all
+// 1024 threads on each, in rounds of up to kBigList pages.
+constexpr int kBigList = 256;
+__device__ void plan_parts(JobDev& job, int np, bool fail, const PageDev* pp, const HStream* streams,
+                           const BlockDesc* blks, int* ctr, PartRec* parts, int64_t cap, int64_t* part) {
   __shared__ int64_t s_base;
-  __shared__ int s_big[1024];  // pages of this round that are split
+  __shared__ int s_fail;
+  __shared__ int s_big[kBigList];
+  __shared__ int64_t s_boff[kBigList];
   __shared__ int s_nbig;
-  JobDev& job = jobs[blockIdx.x];
-  int np = job.num_pages < job.page_cap ? job.num_pages : job.page_cap;
-  if (job.status == kCAPACITY) np = 0;
-  const PageDev* pp = pages + job.page_base;
-  auto nparts = [&](int i, int64_t* count, bool* hyb) -> int64_t {
-    const int64_t c = part_count(pp[i], streams, hyb);
-    *count = c;
-    if (c < 0) return 0;
-    return c > kSplitMin ? (c + kPart - 1) / kPart : 1;
-  };
-  // pass 1: parts per page, the job's slot range
-  int64_t tot_all = 0;
-  for (int b = 0; b < np; b += 1024) {
-    const int i = b + (int)threadIdx.x;
+  if (fail) np = 0;
+  const int seg = (np + 1023) / 1024;
+  const int s0 = (int)threadIdx.x * seg, s1 = s0 + seg < np ? s0 + seg : np;
+  int64_t sum = 0;
+  for (int i = s0; i < s1; i++) {
     int64_t c;
     bool h;
-    const int64_t k = i < np ? nparts(i, &c, &h) : 0;
-    int64_t tot;
-    block_excl_scan<1024>(k, &tot, part);
-    tot_all += tot;
+    sum += part_n(pp[i], streams, &c, &h);
   }
+  int64_t tot;
+  int64_t off = block_excl_scan<1024>(sum, &tot, part);
   if (threadIdx.x == 0) {
-    int64_t base = atomicAdd(ctr + kCtrItems, (int)tot_all);
-    if (base + tot_all > cap) {
-      job.status = kCAPACITY;
-      tot_all = 0;
-    }
+    const int64_t base = fail ? 0 : atomicAdd(ctr + kCtrItems, (int)tot);
+    s_fail = fail || base + tot > cap;
+    if (!fail && s_fail) job.status = kCAPACITY;
     job.item_base = base;
-    job.n_items = (int32_t)tot_all;
+    job.n_items = s_fail ? 0 : (int32_t)tot;
     s_base = base;
   }
   __syncthreads();
-  if (job.status == kCAPACITY) return;
+  if (s_fail) return;
   const int64_t base = s_base;
-  // pass 2: single-part pages; the split ones are listed for pass 3
-  int64_t carry = 0;
-  for (int b = 0; b < np; b += 1024) {
-    const int i = b + (int)threadIdx.x;
-    int64_t c = 0;
-    bool h = false;
-    const int64_t k = i < np ? nparts(i, &c, &h) : 0;
-    int64_t tot;
-    const int64_t ex = carry + block_excl_scan<1024>(k, &tot, part);
-    carry += tot;
+  int cur = s0;
+  for (;;) {
     if (threadIdx.x == 0) s_nbig = 0;
     __syncthreads();
-    if (k == 1) {
-      PartRec r;
-      r.pidx = (int32_t)(job.page_base + i);
-      r.p = 0;
-      r.np = 1;
-      r.v0 = 0;
-      r.b0 = 0;
-      r.vmode = pp[i].vmode;
-      r.chars = r.cstart = r.prel = 0;
-      parts[base + ex] = r;
-    } else if (k > 1) {
-      s_big[atomicAdd(&s_nbig, 1)] = i;
+    // this thread's pages from its cursor: single parts written, split pages
+    // listed (a full list stops the thread at that page, for the next round)
+    for (; cur < s1; cur++) {
+      int64_t c;
+      bool h;
+      const int64_t k = part_n(pp[cur], streams, &c, &h);
+      if (k == 1) {
+        PartRec r;
+        r.pidx = (int32_t)(job.page_base + cur);
+        r.p = 0;
+        r.np = 1;
+        r.v0 = 0;
+        r.b0 = 0;
+        r.vmode = pp[cur].vmode;
+        r.chars = r.cstart = r.prel = 0;
+        parts[base + off] = r;
+      } else if (k > 1) {
+        const int slot = atomicAdd(&s_nbig, 1);
+        if (slot >= kBigList) break;
+        s_big[slot] = cur;
+        s_boff[slot] = off;
+      }
+      off += k;
     }
     __syncthreads();
-    // pass 3: the split pages of this round, every thread on each
-    const int nbig = s_nbig;
+    const int nbig = s_nbig < kBigList ? s_nbig : kBigList;
     for (int q = 0; q < nbig; q++) {
       const int pi = s_big[q];
+      const int64_t poff = s_boff[q];
       int64_t cnt;
       bool hyb;
-      const int64_t P = nparts(pi, &cnt, &hyb);
-      // the page's first slot: its exclusive offset (recomputed: pages before it in this round)
-      __shared__ int64_t s_off;
-      if (i == pi) s_off = ex;
-      __syncthreads();
-      const int64_t off = s_off;
-      __syncthreads();
       const PageDev& pg = pp[pi];
+      const int64_t P = part_n(pg, streams, &cnt, &hyb);
       PartRec r;
       r.pidx = (int32_t)(job.page_base + pi);
       r.np = (int32_t)P;
@@ -1392,7 +1402,7 @@ __global__ void __launch_bounds__(1024) k_part_plan(JobDev* jobs, const PageDev*
           r.p = (int32_t)p;
           r.v0 = (uint32_t)(p * kPart);
           r.b0 = 0;
-          parts[base + off + p] = r;
+          parts[base + poff + p] = r;
         }
       } else {
         // part q starts at the first block whose first value is >= q kPart
@@ -1412,12 +1422,12 @@ __global__ void __launch_bounds__(1024) k_part_plan(JobDev* jobs, const PageDev*
             r.p = (int32_t)p;
             r.v0 = p == 0 ? 0u : (bi < nb && (int64_t)B[bi].v0 < cnt ? B[bi].v0 : (uint32_t)cnt);
             r.b0 = bi;
-            parts[base + off + p] = r;
+            parts[base + poff + p] = r;
           }
         }
       }
     }
-    __syncthreads();
+    if (!__syncthreads_or(cur < s1)) break;
   }
 }
 

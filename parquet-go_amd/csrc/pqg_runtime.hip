@@ -62,9 +62,8 @@ __global__ void k_level_long(PageDev* pages, const int* ctr, const LongLev* long
 __global__ void k_hybrid_walk(const PageDev* pages, const int* list, const int* total, HStream* streams,
                               RunEnt* runs, BlockDesc* blks, LongWalk* longs, int long_cap);
 __global__ void k_walk_long(const int* ctr, const LongWalk* longs, int long_cap, BlockDesc* blks);
-__global__ void k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch);
-__global__ void k_part_plan(JobDev* jobs, const PageDev* pages, const HStream* streams, const BlockDesc* blks,
-                            int* ctr, PartRec* parts, int64_t cap);
+__global__ void k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch, const HStream* streams, const BlockDesc* blks,
+                          int* ctr, PartRec* parts, int64_t parts_cap);
 template <int Mode>
 __global__ void k_values(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total, int* queue,
                          uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks);
@@ -561,9 +560,8 @@ static int launch_pipeline(pqg_ctx* c) {
   hipLaunchKernelGGL(k_walk_long, dim3(c->num_cus * 2), dim3(256), 0, s, ctr, wlong, wlc, blks);
   if (c->timed) hipEventRecord(c->ev[5], s);
   if (c->timed) hipEventRecord(c->ev[6], s);
-  hipLaunchKernelGGL(k_nn_scan, dim3(n), dim3(1024), 0, s, jobs, pages, scratch);
   PartRec* parts = (PartRec*)c->parts.p;
-  hipLaunchKernelGGL(k_part_plan, dim3(n), dim3(1024), 0, s, jobs, pages, streams, blks, ctr, parts, c->parts_cap);
+  hipLaunchKernelGGL(k_nn_scan, dim3(n), dim3(1024), 0, s, jobs, pages, scratch, streams, blks, ctr, parts, c->parts_cap);
   if (c->timed) hipEventRecord(c->ev[7], s);
   // every values kernel takes the work items (the pages' parts) and keeps the
   // ones whose vmode (set by k_page_levels) is its own

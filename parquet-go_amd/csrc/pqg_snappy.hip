@@ -67,14 +67,21 @@ constexpr int kSnFlush = kRing / 4 < 16384 ? kRing / 4 : 16384;
 static_assert((kRing & (kRing - 1)) == 0 && kRing >= 8192, "ring: a power of two >= 8 KiB");
 constexpr int kLongPiece = 4096;  // literal piece read from HBM
 constexpr int kWinLit = 1024;     // literals up to this many bytes (after the granule prefix) move from the window
+#ifndef PQG_SNAPPY_BATCH_WIN
+#define PQG_SNAPPY_BATCH_WIN 3
+#endif
+constexpr int kBatchWin = PQG_SNAPPY_BATCH_WIN;  // windows of kPos positions one batch may take
+constexpr int kBatchTags = 256;   // tag entries of a batch (>= 64 kBatchWin; marks are 1 + entry in a byte)
+constexpr int kBatchRoom = 192;   // a batch with fewer free output bytes takes no further window
+static_assert(64 * kBatchWin < kBatchTags && kBatchTags <= 256, "batch tags: byte marks");
 
 struct SnapShared {
   uint8_t ring[kRing];
   uint8_t in[kSnWin + 32];
   int32_t src[kSpan];     // per output byte: [pre, kSpan) same batch, >= kSpan window byte + kSpan, else history
   uint8_t tmap[kSpan];    // 1 + tag position, at the tag's first output byte
-  u32x2_t tent[kPos];     // per tag position: {output start (relative to the batch's first granule),
-                          //  literal: 0x80000000 | window offset of its bytes; copy: offset}
+  u32x2_t tent[kBatchTags];  // per batch tag: {output start (relative to the batch's first granule),
+                             //  literal: 0x80000000 | window offset of its bytes; copy: offset}
   uint8_t cflag[kPos];    // chain marks of the pointer-doubling walk
 };
 
@@ -539,120 +546,149 @@ struct SnapBlock {
         serial_next = 0;
         continue;
       }
-      // ---- 1. speculative tags at positions lane and 64 + lane
-      const uint32_t wo = (uint32_t)(s - in_base) + lane;
-      const Tag t0 = parse_tag(IN, wo, s + lane, slen, lane);
-      const Tag t1 = parse_tag(IN, wo + 64, s + 64 + lane, slen, 64 + lane);
-      const int n0 = (t0.err || t0.next >= kPos) ? kPos : (int)t0.next;
-      const int n1 = (t1.err || t1.next >= kPos) ? kPos : (int)t1.next;
-      // ---- 2. the chain (pointer doubling, pqg_device.h); tags start before
-      // the end of the block
-      uint64_t cm0, cm1;
-      chain_marks128(n0, n1, lds_ptr(sh->cflag), cm0, cm1);
-      const int64_t lim64 = slen - s;
-      const int lim = lim64 < kPos ? (int)lim64 : kPos;
-      if (lim < 64) {
-        cm0 &= (1ull << lim) - 1;
-        cm1 = 0;
-      } else if (lim < kPos) {
-        cm1 &= (1ull << (lim - 64)) - 1;
-      }
-      const int last = cm1 ? 127 - __builtin_clzll(cm1) : 63 - __builtin_clzll(cm0);
-      const bool on0 = (cm0 >> lane) & 1, on1 = (cm1 >> lane) & 1;
-      PQG_ST(tc);
-      PQG_SA(1, tc - tb);
-      // ---- 3. output offsets and the reference's checks
-      const uint32_t o0 = on0 ? (uint32_t)(t0.len < (1 << 30) ? t0.len : (1 << 30)) : 0u;
-      const uint32_t o1 = on1 ? (uint32_t)(t1.len < (1 << 30) ? t1.len : (1 << 30)) : 0u;
-      const uint32_t i0 = dpp_incl_add(o0);
-      const uint32_t tot0 = (uint32_t)__builtin_amdgcn_readlane((int)i0, 63);
-      const uint32_t i1 = dpp_incl_add(o1) + tot0;
-      const int64_t st0 = (int64_t)(i0 - o0), st1 = (int64_t)(i1 - o1);  // output offsets (relative to d)
+      // A batch: up to kBatchWin windows of kPos positions whose chain tags
+      // fill <= kSpan output bytes, resolved together (step 4a).
       const int64_t a0 = d & ~(int64_t)15;
       const int pre = (int)(d - a0);
-      auto check = [&](const Tag& t, int64_t st, int64_t pos, bool& cut) {
-        const int64_t dt = d + st;
-        const bool past = !lastsub && dt >= dend;                       // the next sub-block's tag
-        bool e = !past && (t.err || t.len > dend - dt);                 // length > len(dst)-d
-        if (!t.lit) e |= !past && (t.info == 0 || (int64_t)t.info > dt - base);  // offset <= 0 || d < offset
-        cut = past || pre + st + t.len > kSpan || (t.lit && pos + t.hdr + t.len > in_base + kSnWin);
-        return e;
-      };
-      bool c0, c1;
-      const bool e0 = check(t0, st0, s + lane, c0), e1 = check(t1, st1, s + 64 + lane, c1);
-      if (__ballot(on0 && e0) | __ballot(on1 && e1)) return kSNAPPY;
-      const uint64_t cb0 = __ballot(on0 && c0), cb1 = __ballot(on1 && c1);
-      const int cutpos = cb0 ? __ffsll((long long)cb0) - 1 : cb1 ? 64 + __ffsll((long long)cb1) - 1 : kPos;
-      if (cutpos == 0) {
-        // tag 0 alone is too long for a batch: a literal (copies are <= 64 bytes)
-        const int64_t l0 = readlane64(t0.len, 0);
-        const int64_t at0 = s + __builtin_amdgcn_readlane(t0.hdr, 0);
-        long_literal(at0, l0);
-        s = at0 + l0;
-        serial_next = 64;
-        continue;
-      }
-      // ---- the chain's tags before cutpos; output [d, d1)
-      const bool b0 = on0 && lane < cutpos, b1 = on1 && 64 + lane < cutpos;
-      const uint64_t bm0 = __ballot(b0), bm1 = __ballot(b1);
-      int64_t out, s1;
-      if (cutpos < kPos) {
-        const int l = cutpos & 63;
-        out = cutpos < 64 ? (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(i0 - o0), l)
-                          : (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(i1 - o1), l);
-        s1 = s + cutpos;
-      } else {
-        out = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)i1, 63);
-        s1 = s + readlane64(last < 64 ? t0.next : t1.next, last & 63);
-      }
-      const int64_t d1 = d + out;
-      PQG_ST(td);
-      PQG_SA(2, td - tc);
-      if (__popcll(bm0) + __popcll(bm1) < kDense) {
-        PQG_SA(10, 1);
-        // ---- 4b. sparse: tag by tag, with the fields already parsed
-        uint64_t m0 = bm0, m1 = bm1;
-        while (m0 | m1) {
-          const bool hi = m0 == 0;
-          const int l = __ffsll((long long)(hi ? m1 : m0)) - 1;
-          if (hi) m1 &= m1 - 1;
-          else m0 &= m0 - 1;
-          const int64_t len = readlane64(hi ? t1.len : t0.len, l);
-          const bool lit = __builtin_amdgcn_readlane((int)(hi ? t1.lit : t0.lit), l) != 0;
-          if (lit) {
-            const int64_t at = s + (hi ? 64 : 0) + l + __builtin_amdgcn_readlane(hi ? t1.hdr : t0.hdr, l);
-            if ((d & 15) + len <= kWinLit) window_literal((uint32_t)(at - in_base), len);
-            else long_literal(at, len);
-          } else {
-            copy_bytes((uint32_t)__builtin_amdgcn_readlane((int)(hi ? t1.info : t0.info), l), (int)len);
-          }
-          maybe_flush();
-        }
-        s = s1;
-        if ((d & ~(int64_t)15) - flushed >= kSnFlush) flush(d & ~(int64_t)15);
-        serial_next = 64;  // a tag-sparse stretch: continue tag by tag
-        PQG_ST(tsp);
-        PQG_SA(3, tsp - td);
-        continue;
-      }
-      PQG_SA(9, 1);
-      PQG_SA(12, __popcll(bm0) + __popcll(bm1));
-      // ---- 4a. dense: per-byte sources for the granules from a0
-      const int end = pre + (int)out;  // batch bytes [pre, end)
+      int filled = pre;  // batch bytes [0, filled) from a0: history prefix + the tags so far
+      int ntag = 0, nwin = 0;
+      bool sparse_done = false;
       PQG_L uint8_t* TM = lds_ptr(sh->tmap);
-      *(PQG_L u32x4_t*)(TM + 16 * lane) = u32x4_t{0u, 0u, 0u, 0u};
-      __builtin_amdgcn_wave_barrier();
       PQG_L u32x2_t* TE = lds_ptr(sh->tent);
-      if (b0) {
-        TE[lane] = u32x2_t{(uint32_t)(pre + (int)st0),
+      for (;;) {
+        // ---- 1. speculative tags at positions lane and 64 + lane
+        const uint32_t wo = (uint32_t)(s - in_base) + lane;
+        const Tag t0 = parse_tag(IN, wo, s + lane, slen, lane);
+        const Tag t1 = parse_tag(IN, wo + 64, s + 64 + lane, slen, 64 + lane);
+        const int n0 = (t0.err || t0.next >= kPos) ? kPos : (int)t0.next;
+        const int n1 = (t1.err || t1.next >= kPos) ? kPos : (int)t1.next;
+        // ---- 2. the chain (pointer doubling, pqg_device.h); tags start before
+        // the end of the block
+        uint64_t cm0, cm1;
+        chain_marks128(n0, n1, lds_ptr(sh->cflag), cm0, cm1);
+        const int64_t lim64 = slen - s;
+        const int lim = lim64 < kPos ? (int)lim64 : kPos;
+        if (lim < 64) {
+          cm0 &= (1ull << lim) - 1;
+          cm1 = 0;
+        } else if (lim < kPos) {
+          cm1 &= (1ull << (lim - 64)) - 1;
+        }
+        const int last = cm1 ? 127 - __builtin_clzll(cm1) : 63 - __builtin_clzll(cm0);
+        const bool on0 = (cm0 >> lane) & 1, on1 = (cm1 >> lane) & 1;
+        PQG_ST(tc);
+        PQG_SA(1, tc - tb);
+        // ---- 3. output offsets (from the batch's current end) and the reference's checks
+        const uint32_t o0 = on0 ? (uint32_t)(t0.len < (1 << 30) ? t0.len : (1 << 30)) : 0u;
+        const uint32_t o1 = on1 ? (uint32_t)(t1.len < (1 << 30) ? t1.len : (1 << 30)) : 0u;
+        const uint32_t i0 = dpp_incl_add(o0);
+        const uint32_t tot0 = (uint32_t)__builtin_amdgcn_readlane((int)i0, 63);
+        const uint32_t i1 = dpp_incl_add(o1) + tot0;
+        const int64_t st0 = (int64_t)(i0 - o0), st1 = (int64_t)(i1 - o1);  // output offsets (relative to a0 + filled)
+        const int64_t dcur = a0 + filled;
+        auto check = [&](const Tag& t, int64_t st, int64_t pos, bool& cut) {
+          const int64_t dt = dcur + st;
+          const bool past = !lastsub && dt >= dend;                       // the next sub-block's tag
+          bool e = !past && (t.err || t.len > dend - dt);                 // length > len(dst)-d
+          if (!t.lit) e |= !past && (t.info == 0 || (int64_t)t.info > dt - base);  // offset <= 0 || d < offset
+          cut = past || filled + st + t.len > kSpan || (t.lit && pos + t.hdr + t.len > in_base + kSnWin);
+          return e;
+        };
+        bool c0, c1;
+        const bool e0 = check(t0, st0, s + lane, c0), e1 = check(t1, st1, s + 64 + lane, c1);
+        if (__ballot(on0 && e0) | __ballot(on1 && e1)) return kSNAPPY;
+        const uint64_t cb0 = __ballot(on0 && c0), cb1 = __ballot(on1 && c1);
+        const int cutpos = cb0 ? __ffsll((long long)cb0) - 1 : cb1 ? 64 + __ffsll((long long)cb1) - 1 : kPos;
+        if (cutpos == 0) {
+          if (nwin > 0) break;  // the batch so far is resolved first
+          // tag 0 alone is too long for a batch: a literal (copies are <= 64 bytes)
+          const int64_t l0 = readlane64(t0.len, 0);
+          const int64_t at0 = s + __builtin_amdgcn_readlane(t0.hdr, 0);
+          long_literal(at0, l0);
+          s = at0 + l0;
+          serial_next = 64;
+          sparse_done = true;
+          break;
+        }
+        // ---- the chain's tags before cutpos; output [dcur, dcur + out)
+        const bool b0 = on0 && lane < cutpos, b1 = on1 && 64 + lane < cutpos;
+        const uint64_t bm0 = __ballot(b0), bm1 = __ballot(b1);
+        int64_t out, s1;
+        if (cutpos < kPos) {
+          const int l = cutpos & 63;
+          out = cutpos < 64 ? (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(i0 - o0), l)
+                            : (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(i1 - o1), l);
+          s1 = s + cutpos;
+        } else {
+          out = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)i1, 63);
+          s1 = s + readlane64(last < 64 ? t0.next : t1.next, last & 63);
+        }
+        PQG_ST(td);
+        PQG_SA(2, td - tc);
+        const int cnt = __popcll(bm0) + __popcll(bm1);
+        if (nwin == 0 && cnt < kDense) {
+          PQG_SA(10, 1);
+          // ---- 4b. sparse: tag by tag, with the fields already parsed
+          uint64_t m0 = bm0, m1 = bm1;
+          while (m0 | m1) {
+            const bool hi = m0 == 0;
+            const int l = __ffsll((long long)(hi ? m1 : m0)) - 1;
+            if (hi) m1 &= m1 - 1;
+            else m0 &= m0 - 1;
+            const int64_t len = readlane64(hi ? t1.len : t0.len, l);
+            const bool lit = __builtin_amdgcn_readlane((int)(hi ? t1.lit : t0.lit), l) != 0;
+            if (lit) {
+              const int64_t at = s + (hi ? 64 : 0) + l + __builtin_amdgcn_readlane(hi ? t1.hdr : t0.hdr, l);
+              if ((d & 15) + len <= kWinLit) window_literal((uint32_t)(at - in_base), len);
+              else long_literal(at, len);
+            } else {
+              copy_bytes((uint32_t)__builtin_amdgcn_readlane((int)(hi ? t1.info : t0.info), l), (int)len);
+            }
+            maybe_flush();
+          }
+          s = s1;
+          if ((d & ~(int64_t)15) - flushed >= kSnFlush) flush(d & ~(int64_t)15);
+          serial_next = 64;  // a tag-sparse stretch: continue tag by tag
+          PQG_ST(tsp);
+          PQG_SA(3, tsp - td);
+          sparse_done = true;
+          break;
+        }
+        if (nwin == 0) {
+          *(PQG_L u32x4_t*)(TM + 16 * lane) = u32x4_t{0u, 0u, 0u, 0u};
+          __builtin_amdgcn_wave_barrier();
+        }
+        // this window's tags: entries ntag.. in chain order (marks 1 + entry at
+        // the tag's first output byte)
+        const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+        const int r0 = ntag + __popcll(bm0 & below), r1 = ntag + __popcll(bm0) + __popcll(bm1 & below);
+        if (b0) {
+          TE[r0] = u32x2_t{(uint32_t)(filled + (int)st0),
                            t0.lit ? (0x80000000u | (uint32_t)(s + lane + t0.hdr - in_base)) : t0.info};
-        TM[pre + st0] = (uint8_t)(lane + 1);
+          TM[filled + st0] = (uint8_t)(r0 + 1);
+        }
+        if (b1) {
+          TE[r1] = u32x2_t{(uint32_t)(filled + (int)st1),
+                           t1.lit ? (0x80000000u | (uint32_t)(s + 64 + lane + t1.hdr - in_base)) : t1.info};
+          TM[filled + st1] = (uint8_t)(r1 + 1);
+        }
+        ntag += cnt;
+        filled += (int)out;
+        s = s1;
+        nwin++;
+        // another window into the same batch: the whole window was taken, room
+        // is left, and its positions (and most literals) are in the LDS window
+        if (cutpos < kPos || nwin >= kBatchWin || filled > kSpan - kBatchRoom || s >= slen ||
+            s + kSnWinNeed / 2 > in_base + kSnWin || (!lastsub && a0 + filled >= dend))
+          break;
       }
-      if (b1) {
-        TE[64 + lane] = u32x2_t{(uint32_t)(pre + (int)st1),
-                                t1.lit ? (0x80000000u | (uint32_t)(s + 64 + lane + t1.hdr - in_base)) : t1.info};
-        TM[pre + st1] = (uint8_t)(65 + lane);
-      }
+      if (sparse_done) continue;
+      PQG_ST(td);
+      PQG_SA(9, 1);
+      PQG_SA(12, ntag);
+      // ---- 4a. dense: per-byte sources for the granules from a0
+      const int end = filled;  // batch bytes [pre, end)
+      const int64_t d1 = a0 + filled;
       __builtin_amdgcn_wave_barrier();
       // tag of each of this lane's 16 bytes: running max of the marks, then
       // the exclusive max over the lanes before
@@ -672,7 +708,7 @@ struct SnapBlock {
       for (int k = 0; k < 16; k++) {
         const int idx = 16 * lane + k;
         const uint32_t t = (tix[k] > before ? tix[k] : before) - 1;
-        const u32x2_t te = TE[t & (kPos - 1)];  // one load for both fields: no load under a branch
+        const u32x2_t te = TE[t & (kBatchTags - 1)];  // one load for both fields: no load under a branch
         const int32_t st = (int32_t)te.x;
         const uint32_t inf = te.y;
         const int32_t v = (inf & 0x80000000u) ? kSpan + (int32_t)(inf & 0x7fffffffu) + (idx - st) : idx - (int32_t)inf;
@@ -681,6 +717,28 @@ struct SnapBlock {
       }
       PQG_ST(te);
       PQG_SA(4, te - td);
+      // Sources older than the ring (copy offsets past kRing, ~20 % of C4's
+      // copies): the flushed output through L2 (sc1 loads bypass this CU's L1,
+      // whose lines may predate later stores), issued now so that their
+      // latency runs under the pointer doubling.  Only this wave's flush
+      // stores need to have landed; the previous batch's went out a batch ago,
+      // and this batch's pending output is flushed after these loads.
+      const int64_t ring_lo = ((d + 15) & ~(int64_t)15) - kRing;
+      uint32_t fm = 0;  // bytes whose (terminal) source is far
+#pragma unroll
+      for (int k = 0; k < 16; k++) fm |= (own[k] < pre && a0 + own[k] < ring_lo) ? 1u << k : 0u;
+      uint32_t fw[16];
+      const bool any_far = __ballot(fm != 0) != 0;
+      if (any_far) {
+        PQG_SA(14, 1);
+        __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+        for (int k = 0; k < 16; k++) {  // unconditional loads (non-far bytes read the output's first dword)
+          const int64_t h = (fm >> k) & 1 ? a0 + own[k] : 0;
+          fw[k] = ld_l2_u32((const PQG_G uint32_t*)((uintptr_t)(dst + h) & ~(uintptr_t)3));
+        }
+      }
+      maybe_flush();  // the output before this batch
       // same-batch copy sources: pointer doubling over src[]
       bool chase = false;
 #pragma unroll
@@ -712,37 +770,34 @@ struct SnapBlock {
       PQG_SA(5, tf - te);
       // every byte reads its source once: the window or the ring (one LDS
       // byte load at a computed address), or, older than the ring, L2
-      const int64_t ring_lo = ((d + 15) & ~(int64_t)15) - kRing;
       const PQG_L uint8_t* shb = (const PQG_L uint8_t*)lds_ptr(sh->ring);  // the ring is at offset 0
       const uint32_t in_off = (uint32_t)(IN - shb);
       uint32_t bt[16];
-      bool far = false;
+      uint32_t fm2 = 0;  // far sources found by the doubling (a copy of a far copy in this batch)
 #pragma unroll
       for (int k = 0; k < 16; k++) {
         const int32_t v = own[k];
         const int64_t h = a0 + v;
         const uint32_t off = v >= kSpan ? in_off + (uint32_t)(v - kSpan) : (uint32_t)(h & (kRing - 1));
-        far |= v < kSpan && h < ring_lo;
+        fm2 |= (v < kSpan && h < ring_lo && !((fm >> k) & 1)) ? 1u << k : 0u;
         bt[k] = shb[off];
       }
-      if (__ballot(far)) {
-        PQG_SA(14, 1);
-        // flushed output, read from L2 (sc1 loads bypass this CU's L1, whose
-        // lines may predate later stores): only this wave's flush stores need
-        // to have landed
+      if (any_far) {
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+          if ((fm >> k) & 1) bt[k] = (fw[k] >> (((uintptr_t)(dst + a0 + own[k]) & 3) * 8)) & 0xff;
+      }
+      if (__ballot(fm2 != 0)) {
+        PQG_SA(13, 1000000);
         __builtin_amdgcn_s_waitcnt(0);
-        uint32_t fw[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) {
-          const int64_t h = a0 + own[k];
-          const bool f = own[k] < kSpan && h < ring_lo;
-          fw[k] = f ? ld_l2_u32((const PQG_G uint32_t*)((uintptr_t)(dst + h) & ~(uintptr_t)3)) : 0u;
+          const int64_t h = (fm2 >> k) & 1 ? a0 + own[k] : 0;
+          fw[k] = ld_l2_u32((const PQG_G uint32_t*)((uintptr_t)(dst + h) & ~(uintptr_t)3));
         }
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-          const int64_t h = a0 + own[k];
-          if (own[k] < kSpan && h < ring_lo) bt[k] = (fw[k] >> (((uintptr_t)(dst + h) & 3) * 8)) & 0xff;
-        }
+        for (int k = 0; k < 16; k++)
+          if ((fm2 >> k) & 1) bt[k] = (fw[k] >> (((uintptr_t)(dst + a0 + own[k]) & 3) * 8)) & 0xff;
       }
       __builtin_amdgcn_wave_barrier();
       if (16 * lane < end) {
@@ -752,9 +807,7 @@ struct SnapBlock {
         sts16(lds_ptr(sh->ring) + ((a0 + 16 * lane) & (kRing - 1)), make_uint4(w[0], w[1], w[2], w[3]));
       }
       __builtin_amdgcn_wave_barrier();
-      d = d1;
-      s = s1;
-      maybe_flush();
+      d = d1;  // flushed by the next batch (after its far loads) or the next path
       PQG_ST(tg);
       PQG_SA(6, tg - tf);
     }

@@ -667,7 +667,8 @@ __global__ void __launch_bounds__(64) k_str_delta(JobDev* jobs, PageDev* pages, 
           if ((lane & 7) >= o) incl += tt;
         }
         my_send = send + incl;
-        const int64_t eff_pl = dba && pl > 0 ? pl : 0;
+        // (lanes past the values read the streams' miniblock padding: no bytes)
+        const int64_t eff_pl = live && i < cnt && dba && pl > 0 ? pl : 0;
         my_len = eff_pl + s64;
         int64_t li = my_len;
 #pragma unroll

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 session 7: GPU inflate (k_inflate) parity, the whole -m gpu suite,
-# C2 / C2 run-heavy with the wave level decoder back as the only one.
+# C2 / C2 run-heavy with the wave level decoder back as the only one, part
+# planning folded into k_nn_scan.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gzip.py tests/test_boundary.py -m gpu -x -v --timeout 120 --timeout-method thread \
