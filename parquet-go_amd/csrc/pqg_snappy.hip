@@ -64,9 +64,16 @@ constexpr int kRing = PQG_SNAPPY_RING;  // output history kept in LDS (a power o
 // flush granularity (a wave's stores are waited for at the next loop head);
 // unflushed bytes (< kSnFlush + a batch or literal piece) must stay inside the ring
 constexpr int kSnFlush = kRing / 4 < 16384 ? kRing / 4 : 16384;
-static_assert((kRing & (kRing - 1)) == 0 && kRing >= 8192, "ring: a power of two >= 8 KiB");
-constexpr int kLongPiece = 4096;  // literal piece read from HBM
+// (kSnFlush + two writes of <= kLongPiece / a batch must fit the ring)
+static_assert((kRing & (kRing - 1)) == 0 && kRing >= 4096, "ring: a power of two >= 4 KiB");
+constexpr int kLongPiece = kRing >= 8192 ? 4096 : 1024;  // literal piece read from HBM
 constexpr int kWinLit = 1024;     // literals up to this many bytes (after the granule prefix) move from the window
+#ifndef PQG_SNAPPY_WPE
+#define PQG_SNAPPY_WPE 1  // waves per EU the decoder is compiled for (3: <= 168 VGPRs)
+#endif
+#ifndef PQG_SNAPPY_SERIAL_CHAIN
+#define PQG_SNAPPY_SERIAL_CHAIN 0
+#endif
 #ifndef PQG_SNAPPY_BATCH_WIN
 #define PQG_SNAPPY_BATCH_WIN 3
 #endif
@@ -78,12 +85,17 @@ static_assert(64 * kBatchWin < kBatchTags && kBatchTags <= 256, "batch tags: byt
 struct SnapShared {
   uint8_t ring[kRing];
   uint8_t in[kSnWin + 32];
-  int32_t src[kSpan];     // per output byte: [pre, kSpan) same batch, >= kSpan window byte + kSpan, else history
-  uint8_t tmap[kSpan];    // 1 + tag position, at the tag's first output byte
-  u32x2_t tent[kBatchTags];  // per batch tag: {output start (relative to the batch's first granule),
-                             //  literal: 0x80000000 | window offset of its bytes; copy: offset}
+  union {
+    int32_t src[kSpan];  // per output byte: [pre, kSpan) same batch, >= kSpan window byte + kSpan, else history
+    struct {             // (before the doubling, which is the only user of src)
+      uint8_t tmap[kSpan];         // 1 + batch tag entry, at the tag's first output byte
+      u32x2_t tent[kBatchTags];    // per batch tag: {output start (relative to the batch's first granule),
+                                   //  literal: 0x80000000 | window offset of its bytes; copy: offset}
+    };
+  };
   uint8_t cflag[kPos];    // chain marks of the pointer-doubling walk
 };
+static_assert(kSpan + 8 * kBatchTags <= 4 * kSpan, "tmap + tent share src's bytes");
 
 // ---- 64-lane DPP scans (row_shr 1/2/4/8, row_bcast 15/31)
 __device__ __forceinline__ uint32_t dpp_incl_add(uint32_t x) {
@@ -538,7 +550,6 @@ struct SnapBlock {
       PQG_ST(tb);
       PQG_SA(0, tb - ta);
       if (serial_next > 0) {
-        PQG_SA(11, 1);
         const int e = serial(s, serial_next);
         PQG_ST(tsx);
         PQG_SA(7, tsx - tb);
@@ -556,6 +567,7 @@ struct SnapBlock {
       PQG_L uint8_t* TM = lds_ptr(sh->tmap);
       PQG_L u32x2_t* TE = lds_ptr(sh->tent);
       for (;;) {
+        PQG_ST(tw);
         // ---- 1. speculative tags at positions lane and 64 + lane
         const uint32_t wo = (uint32_t)(s - in_base) + lane;
         const Tag t0 = parse_tag(IN, wo, s + lane, slen, lane);
@@ -565,7 +577,23 @@ struct SnapBlock {
         // ---- 2. the chain (pointer doubling, pqg_device.h); tags start before
         // the end of the block
         uint64_t cm0, cm1;
+#if PQG_SNAPPY_SERIAL_CHAIN
+        {  // A/B: the chain by a scalar v_readlane walk
+          cm0 = cm1 = 0;
+          int q = 0;
+          while (q < kPos) {
+            if (q < 64) {
+              cm0 |= 1ull << q;
+              q = __builtin_amdgcn_readlane(n0, q);
+            } else {
+              cm1 |= 1ull << (q - 64);
+              q = __builtin_amdgcn_readlane(n1, q - 64);
+            }
+          }
+        }
+#else
         chain_marks128(n0, n1, lds_ptr(sh->cflag), cm0, cm1);
+#endif
         const int64_t lim64 = slen - s;
         const int lim = lim64 < kPos ? (int)lim64 : kPos;
         if (lim < 64) {
@@ -577,7 +605,7 @@ struct SnapBlock {
         const int last = cm1 ? 127 - __builtin_clzll(cm1) : 63 - __builtin_clzll(cm0);
         const bool on0 = (cm0 >> lane) & 1, on1 = (cm1 >> lane) & 1;
         PQG_ST(tc);
-        PQG_SA(1, tc - tb);
+        PQG_SA(1, tc - tw);
         // ---- 3. output offsets (from the batch's current end) and the reference's checks
         const uint32_t o0 = on0 ? (uint32_t)(t0.len < (1 << 30) ? t0.len : (1 << 30)) : 0u;
         const uint32_t o1 = on1 ? (uint32_t)(t1.len < (1 << 30) ? t1.len : (1 << 30)) : 0u;
@@ -739,6 +767,8 @@ struct SnapBlock {
         }
       }
       maybe_flush();  // the output before this batch
+      PQG_ST(te2);
+      PQG_SA(11, te2 - te);
       // same-batch copy sources: pointer doubling over src[]
       bool chase = false;
 #pragma unroll
@@ -767,7 +797,7 @@ struct SnapBlock {
         }
       }
       PQG_ST(tf);
-      PQG_SA(5, tf - te);
+      PQG_SA(5, tf - te2);
       // every byte reads its source once: the window or the ring (one LDS
       // byte load at a computed address), or, older than the ring, L2
       const PQG_L uint8_t* shb = (const PQG_L uint8_t*)lds_ptr(sh->ring);  // the ring is at offset 0
@@ -788,7 +818,6 @@ struct SnapBlock {
           if ((fm >> k) & 1) bt[k] = (fw[k] >> (((uintptr_t)(dst + a0 + own[k]) & 3) * 8)) & 0xff;
       }
       if (__ballot(fm2 != 0)) {
-        PQG_SA(13, 1000000);
         __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
         for (int k = 0; k < 16; k++) {
@@ -1109,7 +1138,7 @@ __global__ void __launch_bounds__(64) k_snap_link(const JobDev* jobs, PageDev* p
   }
 }
 
-__global__ void __launch_bounds__(64) k_snap_decode(const JobDev* jobs, PageDev* pages, const SnapSub* subs,
+__global__ void __launch_bounds__(64, PQG_SNAPPY_WPE) k_snap_decode(const JobDev* jobs, PageDev* pages, const SnapSub* subs,
                                                     const int* sub_total, int sub_cap, int* queue, uint8_t* scratch) {
   __shared__ __attribute__((aligned(16))) SnapShared sh;
   const int lane = lane_id();
@@ -1144,7 +1173,7 @@ __global__ void __launch_bounds__(64) k_snap_decode(const JobDev* jobs, PageDev*
 
 // The serial path: pages whose split decode failed (k_snap_plan / k_snap_link
 // / k_snap_decode set sn_fallback), decoded from the start on one wave.
-__global__ void __launch_bounds__(64) k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+__global__ void __launch_bounds__(64, PQG_SNAPPY_WPE) k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total,
                                                int* queue, uint8_t* scratch) {
   __shared__ __attribute__((aligned(16))) SnapShared sh;
   const int lane = lane_id();

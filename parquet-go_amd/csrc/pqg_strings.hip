@@ -53,79 +53,46 @@ int prof_read_strings(unsigned long long* out) {
 // Block-parallel length-chain walk (PLAIN byte arrays and byte-array
 // dictionary pages).
 //
-// The chain 0 -> 4 + len(0) -> ... is serial, but it is walked in parallel:
-// the byte range is cut into kWalkT segments, and thread t walks the records
-// that start in segment t, from the first position p of the segment whose
-// chain looks valid for three records (u32 length >= 0 and inside the
-// stream).  A walk is only as good as its start; thread 0 then checks, in
-// order, that each segment's start is the position where the true chain
-// (from byte 0) enters the segment — the exit of the previous segment's walk —
-// and re-walks a segment itself when it is not.  The result is exactly the
-// serial chain whatever the data; the guess only decides how much is re-walked
-// (for text-like records: nothing).  A second pass walks every segment again
-// from its verified start and writes the outputs at their record index.
-//
-// Each thread reads through a 64-byte register window (4 aligned granules):
-// every segment walk is a chain of dependent loads, so the window turns a
-// load per record into a load per ~64 bytes.
+// The chain 0 -> 4 + len(0) -> ... is serial, but it is walked in parallel,
+// 32 KiB of the stream at a time: the chunk is staged in LDS with one round
+// of coalesced loads (the next chunk's loads are in flight meanwhile), each of
+// the 512 threads takes a 64-byte segment, guesses where the chain enters it
+// (the first position whose length chain is valid for three records; the
+// segment holding the known chain position takes that) and walks its records
+// from there, keeping their ends in registers.  The guesses are then checked
+// all at once: every segment's entry must be the exit of the nearest segment
+// before it that holds records (a block max-scan), and the first segment's is
+// the known chain position.  When they all hold, a block scan of the record
+// counts places every record and the ends are written; when one does not (or
+// a record fails), thread 0 walks the chunk's true chain itself.  The result
+// is exactly the serial chain whatever the data; the guess only decides
+// whether the chunk takes the serial walk (for text-like records: never).
 // ---------------------------------------------------------------------------
 constexpr int kWalkT = 512;
-
-__device__ __forceinline__ uint32_t pick4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
-  return (k & 2) ? ((k & 1) ? d : c) : ((k & 1) ? b : a);
-}
-
-// Walk records from `pos` while pos < stop and fewer than `limit` records are
-// done.  Returns the records walked; *end = the position after them, *fail = 1
-// when the record at *end is not valid (length negative or past n, or fewer
-// than 4 bytes left).  sink(k, pos_after) sees record k of the walk.
-template <class F>
-__device__ __forceinline__ uint32_t seg_walk(gcu8 p, uint32_t n, uint32_t pos, uint32_t stop, uint32_t limit,
-                                             uint32_t* end, int* fail, F&& sink) {
-  uintptr_t wb = 0;
-  uint4 g0 = make_uint4(0, 0, 0, 0), g1 = g0, g2 = g0, g3 = g0;
-  const uintptr_t pend = (uintptr_t)(p + n);
-  uint32_t k = 0;
-  *fail = 0;
-  while (pos < stop && k < limit) {
-    if (n - pos < 4) { *fail = 1; break; }
-    const uintptr_t a = (uintptr_t)(p + pos);
-    if (a < wb || a + 4 > wb + 64) {
-      wb = a & ~(uintptr_t)15;
-      // four loads issued together, unconditionally (a guarded load would be
-      // waited for at its branch join): granules past the stream's last one
-      // re-read that one, their bytes are never used
-      const uintptr_t lastg = (pend - 1) & ~(uintptr_t)15;
-      g0 = ldg16(wb);
-      g1 = ldg16(wb + 16 < lastg ? wb + 16 : lastg);
-      g2 = ldg16(wb + 32 < lastg ? wb + 32 : lastg);
-      g3 = ldg16(wb + 48 < lastg ? wb + 48 : lastg);
-    }
-    const uint32_t off = (uint32_t)(a - wb), d = off >> 2, e = d + 1 < 16 ? d + 1 : 15;
-    const uint32_t lo = pick4(pick4(g0.x, g0.y, g0.z, g0.w, d), pick4(g1.x, g1.y, g1.z, g1.w, d),
-                              pick4(g2.x, g2.y, g2.z, g2.w, d), pick4(g3.x, g3.y, g3.z, g3.w, d), d >> 2);
-    const uint32_t hi = pick4(pick4(g0.x, g0.y, g0.z, g0.w, e), pick4(g1.x, g1.y, g1.z, g1.w, e),
-                              pick4(g2.x, g2.y, g2.z, g2.w, e), pick4(g3.x, g3.y, g3.z, g3.w, e), e >> 2);
-    const uint32_t l = __builtin_amdgcn_alignbit(hi, lo, (off & 3) * 8);
-    if ((int32_t)l < 0 || n - pos - 4 < l) { *fail = 1; break; }
-    pos += 4 + l;
-    sink(k, pos);
-    k++;
-  }
-  *end = pos;
-  return k;
-}
+constexpr int kPwSeg = 64;                  // bytes per thread segment
+constexpr int kPwChunk = kWalkT * kPwSeg;   // bytes per chunk (LDS)
+constexpr int kPwRec = kPwSeg / 4;          // records a segment can hold (>= 4 bytes each)
+constexpr int kPwAhead = 4096;              // staged past the chunk: the guesses' chain checks
+constexpr int kPwStage = kPwChunk + kPwAhead + 64;
+constexpr int kPwG = (kPwStage / 16 + kWalkT - 1) / kWalkT;  // staged granules per thread
 
 struct BlockWalkShared {
-  uint32_t start[kWalkT];  // pass A: first guessed start (0xffffffff: none); pass B: verified start
-  uint32_t exit_[kWalkT];  // position after the segment's records
-  uint32_t cnt[kWalkT];    // records walked
-  uint32_t start2[kWalkT], exit2[kWalkT], cnt2[kWalkT];  // the second guess
-  uint32_t base[kWalkT];   // pass B: index of the segment's first record (0xffffffff: segment unused)
-  uint8_t fail[kWalkT], fail2[kWalkT];
-  uint32_t last_end;       // end of record count-1
+  uint8_t buf[kPwG * kWalkT * 16];  // the chunk from its 16-aligned start, + kPwAhead + 64 bytes
+  uint32_t X[kWalkT];          // per segment: exit (chain position after its records)
+  int64_t part[kWalkT / 64 + 1];
+  int keys[kWalkT / 64];
+  uint32_t cur;                // the true chain position (the first record start not yet placed)
+  uint32_t idx;                // records placed
+  uint32_t last_end;           // end of record count - 1
   int status;
+  int serial;
 };
+
+// u32 at LDS byte offset o (any alignment)
+__device__ __forceinline__ uint32_t lds_u32(const PQG_L uint8_t* b, uint32_t o) {
+  const PQG_L uint32_t* q = (const PQG_L uint32_t*)(b + (o & ~3u));
+  return __builtin_amdgcn_alignbit(q[1], q[0], (o & 3) * 8);
+}
 
 // byteArrayPlainDecoder.next for records [0, count) of [p, p+n), the whole
 // block.  mode 0 (data page): out[i] = char end of value i = end(i) - 4 (i + 1);
@@ -133,155 +100,162 @@ struct BlockWalkShared {
 // Returns the status (all threads); *chars = sum of the lengths.
 __device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out, int mode, int64_t* chars,
                           BlockWalkShared& sh) {
-  const int t = threadIdx.x;
-  const uint32_t L = ((n + kWalkT - 1) / kWalkT + 63) & ~63u;  // segment bytes (>= 64)
-  const uint32_t lo = (uint32_t)t * L < n ? (uint32_t)t * L : n;
-  const uint32_t hi = lo + L < n ? lo + L : n;
-  const uint32_t kNone = 0xffffffffu;
-  auto nop = [](uint32_t, uint32_t) {};
-  PQG_T(tp0);
-  // ---- pass A: guess two starts, walk the segment from each
-  // (a false start is typically the byte before a record — [c, len, 0, 0] reads
-  // as a short length — so the next candidate is usually the true record)
-  if (count > 0) {
-    uint32_t st = kNone, st2 = kNone;
-    if (t == 0) {
-      st = 0;
-    } else {
-      // positions whose length chain is valid for three records; a candidate
-      // is first screened on its own length (one 64-byte window load per 60
-      // positions), the deeper check walks from it
-      uintptr_t wb = 0;
-      uint4 g0 = make_uint4(0, 0, 0, 0), g1 = g0, g2 = g0, g3 = g0;
-      const uintptr_t pend = (uintptr_t)(p + n), lastg = (pend - 1) & ~(uintptr_t)15;
-      for (uint32_t q = lo; q < hi && n - q >= 4; q++) {
-        if (st != kNone && q > st + 64) break;
-        const uintptr_t a = (uintptr_t)(p + q);
-        if (a + 4 > wb + 64) {
-          wb = a & ~(uintptr_t)15;
-          g0 = ldg16(wb);
-          g1 = ldg16(wb + 16 < lastg ? wb + 16 : lastg);
-          g2 = ldg16(wb + 32 < lastg ? wb + 32 : lastg);
-          g3 = ldg16(wb + 48 < lastg ? wb + 48 : lastg);
-        }
-        const uint32_t off = (uint32_t)(a - wb), d = off >> 2, e1 = d + 1 < 16 ? d + 1 : 15;
-        const uint32_t w0 = pick4(pick4(g0.x, g0.y, g0.z, g0.w, d), pick4(g1.x, g1.y, g1.z, g1.w, d),
-                                  pick4(g2.x, g2.y, g2.z, g2.w, d), pick4(g3.x, g3.y, g3.z, g3.w, d), d >> 2);
-        const uint32_t w1 = pick4(pick4(g0.x, g0.y, g0.z, g0.w, e1), pick4(g1.x, g1.y, g1.z, g1.w, e1),
-                                  pick4(g2.x, g2.y, g2.z, g2.w, e1), pick4(g3.x, g3.y, g3.z, g3.w, e1), e1 >> 2);
-        const uint32_t l = __builtin_amdgcn_alignbit(w1, w0, (off & 3) * 8);
-        if ((int32_t)l < 0 || n - q - 4 < l) continue;
-        uint32_t e;
-        int f;
-        const uint32_t k = seg_walk(p, n, q, n, 3, &e, &f, nop);
-        if (k == 3 || (f && e == n)) {
-          if (st == kNone) {
-            st = q;
-          } else {
-            st2 = q;
-            break;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t == 0) {
+    sh.cur = 0;
+    sh.idx = 0;
+    sh.last_end = 0;
+    sh.status = kOK;
+  }
+  const uintptr_t pend = (uintptr_t)(p + n);
+  // granule k of the chunk from c0 (aligned start): mapped when it holds a stream byte
+  auto load_chunk = [&](uint32_t c0, uint4 (&v)[kPwG]) {
+    const uintptr_t A = (uintptr_t)(p + c0) & ~(uintptr_t)15;
+#pragma unroll
+    for (int k = 0; k < kPwG; k++) {
+      const uintptr_t g = A + 16 * (uintptr_t)(t + kWalkT * k);
+      v[k] = (g < pend && g - A < (uintptr_t)kPwStage) ? ldg16(g) : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  uint4 nx[kPwG];
+  if (count > 0) load_chunk(0, nx);
+  __syncthreads();
+  for (uint32_t c0 = 0; count > 0 && c0 < n; c0 += kPwChunk) {
+    const uint32_t c1 = n - c0 > (uint32_t)kPwChunk ? c0 + kPwChunk : n;
+    const uint32_t cur = sh.cur, idx0 = sh.idx;
+    if (idx0 >= count) break;
+    if (cur >= c1) {  // a record spans the chunk
+      if (c1 < n) load_chunk(c1, nx);
+      continue;
+    }
+    // stage this chunk, then start the next one's loads
+#pragma unroll
+    for (int k = 0; k < kPwG; k++) sts16(lds_ptr(sh.buf) + 16 * (t + kWalkT * k), nx[k]);
+    __syncthreads();
+    if (c1 < n) load_chunk(c1, nx);
+    PQG_ACC0(21, 1);
+    const uint32_t off0 = (uint32_t)(((uintptr_t)(p + c0)) & 15);  // buf index of stream position c0
+    const PQG_L uint8_t* B = lds_ptr(sh.buf);
+    auto len_at = [&](uint32_t q) { return lds_u32(B, q - c0 + off0); };  // q + 4 <= c1 + kPwAhead + 48
+    // ---- guess and walk this thread's segment
+    const uint32_t lo = c0 + kPwSeg * (uint32_t)t, hi = lo + kPwSeg < c1 ? lo + kPwSeg : c1;
+    bool has = false, fail = false;
+    uint32_t g = 0, x = 0, k = 0;
+    uint32_t ends[kPwRec];
+    if (lo < hi && cur < hi) {
+      if (cur >= lo) {
+        g = cur;
+        has = true;
+      } else {
+        // every position of the segment is a candidate whose records up to hi
+        // and two more after them (inside the staged bytes, or to the end of
+        // the stream) are valid; the one with the most records in the segment
+        // wins (the true entry starts the longest run: a false start two or
+        // three bytes before a record may jump onto the true chain, but only
+        // after leaving the segment), then the nearest exit
+        uint32_t best_k = 0, best_x = 0xffffffffu;
+        for (uint32_t q = lo; q < hi; q++) {
+          uint32_t r = q, kk = 0;
+          bool ok = true;
+          int extra = 0;
+          while (ok && extra < 2) {
+            if (r == n) break;
+            if (r >= c1 + kPwAhead) break;  // leaves the staged bytes: no further check
+            if (n - r < 4) { ok = false; break; }
+            const uint32_t l = len_at(r);
+            if ((int32_t)l < 0 || n - r - 4 < l) { ok = false; break; }
+            if (r < hi) kk++;
+            else extra++;
+            r += 4 + l;
+          }
+          if (!ok) continue;
+          uint32_t x = q;  // this candidate's exit
+          while (x < hi) x += 4 + len_at(x);  // (validated above)
+          if (kk > best_k || (kk == best_k && x < best_x)) {
+            best_k = kk;
+            best_x = x;
+            g = q;
+            has = true;
           }
         }
       }
-    }
-    sh.start[t] = st;
-    sh.start2[t] = st2;
-    sh.fail[t] = sh.fail2[t] = 0;
-    sh.cnt[t] = sh.cnt2[t] = 0;
-    sh.exit_[t] = st;
-    sh.exit2[t] = st2;
-    uint32_t e;
-    int f;
-    if (st != kNone && st < hi) {
-      sh.cnt[t] = seg_walk(p, n, st, hi, 0xffffffffu, &e, &f, nop);
-      sh.exit_[t] = e;
-      sh.fail[t] = (uint8_t)f;
-    }
-    if (st2 != kNone && st2 < hi) {
-      sh.cnt2[t] = seg_walk(p, n, st2, hi, 0xffffffffu, &e, &f, nop);
-      sh.exit2[t] = e;
-      sh.fail2[t] = (uint8_t)f;
-    }
-  }
-  __syncthreads();
-  PQG_T(tp1);
-  // ---- thread 0: follow the true chain through the segments
-  if (t == 0) {
-    uint32_t redo = 0, redo_k = 0;
-    (void)redo;
-    (void)redo_k;
-    for (int s = 0; s < kWalkT; s++) sh.base[s] = kNone;
-    uint32_t cur = 0, idx = 0;
-    int status = kOK;
-    bool failed = false;
-    for (int s = 0; s < kWalkT && idx < count; s++) {
-      const uint32_t slo = (uint32_t)s * L < n ? (uint32_t)s * L : n;
-      const uint32_t shi = slo + L < n ? slo + L : n;
-      if (shi <= slo) break;     // past the end of the stream
-      if (cur >= shi) continue;  // a record spans the whole segment
-      uint32_t k, e;
-      int f;
-      if (sh.start[s] == cur) {  // a guess was right: take the segment's walk
-        k = sh.cnt[s];
-        e = sh.exit_[s];
-        f = sh.fail[s];
-      } else if (sh.start2[s] == cur) {
-        k = sh.cnt2[s];
-        e = sh.exit2[s];
-        f = sh.fail2[s];
-      } else {
-        k = seg_walk(p, n, cur, shi, 0xffffffffu, &e, &f, nop);
-        redo++;
-        redo_k += k;
-      }
-      sh.start[s] = cur;
-      sh.base[s] = idx;
-      idx += k;
-      cur = e;
-      if (f) {
-        failed = true;
-        break;
+      if (has) {
+        uint32_t pos = g;
+        while (pos < hi) {
+          if (n - pos < 4) { fail = true; break; }
+          const uint32_t l = len_at(pos);
+          if ((int32_t)l < 0 || n - pos - 4 < l) { fail = true; break; }
+          pos += 4 + l;
+#pragma unroll
+          for (int j = 0; j < kPwRec; j++)
+            if ((uint32_t)j == k) ends[j] = pos;
+          k++;
+        }
+        x = pos;
       }
     }
-    if (idx < count) {
-      // record `idx` at `cur` fails: fewer than 4 bytes (EOF), a negative
-      // length, or fewer bytes than its length (EOF)
-      status = kEOF;
-      if (failed && n - cur >= 4) {
-        const uint32_t l = (uint32_t)p[cur] | (uint32_t)p[cur + 1] << 8 | (uint32_t)p[cur + 2] << 16 |
-                           (uint32_t)p[cur + 3] << 24;
-        if ((int32_t)l < 0) status = kBYTE_ARRAY;
-      }
+    // ---- check every guess at once: entry == exit of the nearest segment before with records
+    sh.X[t] = x;
+    int key = has ? t + 1 : 0;  // inclusive max-scan of the segments with records
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(key, o, 64);
+      if (lane >= o) key = y > key ? y : key;
     }
-    sh.status = status;
-    sh.last_end = 0;
-    PQG_ACC0(20, redo);
-    PQG_ACC0(21, redo_k);
+    if (lane == 63) sh.keys[wv] = key;
+    __syncthreads();
+    int before = 0;
+    for (int w = 0; w < wv; w++) before = sh.keys[w] > before ? sh.keys[w] : before;
+    int ex = __shfl_up(key, 1, 64);
+    if (lane == 0) ex = 0;
+    ex = ex > before ? ex : before;               // nearest segment before t with records, + 1
+    const uint32_t P = ex ? sh.X[ex - 1] : cur;  // the chain position entering segment t
+    const bool bad = (lo < hi && cur < hi) && (has ? (g != P || fail) : P < hi);
+    const int any_bad = __syncthreads_or(bad);
+    if (!any_bad) {
+      int64_t tot;
+      const int64_t base = (int64_t)idx0 + block_excl_scan<kWalkT>(has ? (int64_t)k : 0, &tot, sh.part);
+#pragma unroll
+      for (int j = 0; j < kPwRec; j++) {
+        const int64_t i = base + j;
+        if ((uint32_t)j < k && i < (int64_t)count) {
+          out[i] = mode ? (int64_t)ends[j] : (int64_t)ends[j] - 4 * (i + 1);
+          if (i == (int64_t)count - 1) sh.last_end = ends[j];
+        }
+      }
+      // the last segment with records hands the chain on (the exit of the chunk)
+      const int last = __shfl(key, 63, 64);  // this wave's; the block's is the max over waves
+      int blast = 0;
+      for (int w = 0; w < kWalkT / 64; w++) blast = sh.keys[w] > blast ? sh.keys[w] : blast;
+      (void)last;
+      if (t == 0) {
+        sh.idx = idx0 + (uint32_t)(tot < (int64_t)(count - idx0) ? tot : (int64_t)(count - idx0));
+        if (blast) sh.cur = sh.X[blast - 1];
+      }
+    } else if (t == 0) {
+      // the serial walk of the chunk's true chain (exact errors: reference order)
+      PQG_ACC0(20, 1);
+      uint32_t pos = cur, i = idx0;
+      int st = kOK;
+      while (pos < c1 && i < count) {
+        if (n - pos < 4) { st = kEOF; break; }
+        const uint32_t l = len_at(pos);
+        if ((int32_t)l < 0) { st = kBYTE_ARRAY; break; }
+        if (n - pos - 4 < l) { st = kEOF; break; }
+        pos += 4 + l;
+        out[i] = mode ? (int64_t)pos : (int64_t)pos - 4 * ((int64_t)i + 1);
+        if (i == count - 1) sh.last_end = pos;
+        i++;
+      }
+      sh.cur = pos;
+      sh.idx = i;
+      sh.status = st;
+    }
+    __syncthreads();
+    if (sh.status != kOK) return sh.status;
   }
   __syncthreads();
-  PQG_T(tp2);
-  const int status = sh.status;
-  if (status != kOK) return status;
-  // ---- pass B: outputs from the verified starts
-  if (count > 0 && sh.base[t] != kNone && sh.base[t] < count) {
-    const uint32_t b = sh.base[t];
-    uint32_t e;
-    int f;
-    seg_walk(p, n, sh.start[t], hi, count - b, &e, &f,
-             [&](uint32_t k, uint32_t pos) {
-               const uint32_t i = b + k;
-               out[i] = mode ? (int64_t)pos : (int64_t)pos - 4 * ((int64_t)i + 1);
-               if (i == count - 1) sh.last_end = pos;
-             });
-  }
-  __syncthreads();
-  PQG_T(tp3);
-#ifdef PQG_PROFILE
-  PQG_ACC0(16, tp1 - tp0);
-  PQG_ACC0(17, tp2 - tp1);
-  PQG_ACC0(18, tp3 - tp2);
-  PQG_ACC0(19, 1);
-#endif
+  if (sh.idx < count) return kEOF;  // the stream ends before record `idx`
   *chars = count ? (int64_t)sh.last_end - 4 * (int64_t)count : 0;
   return kOK;
 }
@@ -873,18 +847,39 @@ __global__ void __launch_bounds__(256) k_char_scan(JobDev* jobs, PageDev* pages,
 namespace pqg {
 
 // ---- K7d -----------------------------------------------------------------------
-// One block per byte-array data page, one value per thread.  PLAIN: value i's
-// chars [e(i-1), e(i)) come from its record at e(i-1) + 4 (i + 1) of the page's
-// value section (k_str_plain left the page-relative ends in the offsets).
-// Dictionary: the slot holds the key (k_str_count); the value is dictionary
-// entry `key`, and its start is a block scan of the entry lengths.  The ends
-// become chunk offsets.  512 independent copies per block keep many loads in
-// flight.
+// One block per byte-array data page part, one value per thread.  PLAIN: value
+// i's chars [e(i-1), e(i)) come from its record at e(i-1) + 4 (i + 1) of the
+// page's value section (k_str_plain left the page-relative ends in the
+// offsets).  Dictionary: the slot holds the key (k_str_count); the value is
+// dictionary entry `key`, and its start is a block scan of the entry lengths.
+// The ends become chunk offsets.  A round's 512 values are assembled in LDS
+// and leave as aligned 16-byte granules (only the round's two edge granules,
+// shared with the neighbouring rounds or pages, are written bytewise); a round
+// of more than kCopyStage bytes copies value by value.
+constexpr int kCopyStage = 16384;
+
+// len bytes from global src to LDS dst (any alignment)
+__device__ __forceinline__ void lds_copy(PQG_L uint8_t* dst, gcu8 src, int64_t len) {
+  int64_t k = 0;
+  for (; k + 4 <= len; k += 4) {
+    const uintptr_t a = (uintptr_t)(src + k);
+    const PQG_G uint32_t* q = (const PQG_G uint32_t*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3) * 8;
+    const uint32_t x = sh ? __builtin_amdgcn_alignbit(q[1], q[0], sh) : q[0];
+    dst[k] = (uint8_t)x;
+    dst[k + 1] = (uint8_t)(x >> 8);
+    dst[k + 2] = (uint8_t)(x >> 16);
+    dst[k + 3] = (uint8_t)(x >> 24);
+  }
+  for (; k < len; k++) dst[k] = src[k];
+}
+
 __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total,
                                                   int* queue, uint8_t* value_arena, int64_t* offs_arena) {
   __shared__ int s_t;
   __shared__ int64_t s_prev;  // page-relative end of the value before the round
   __shared__ int64_t part[9];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kCopyStage];
   const int n_items = total[kCtrItems];
   for (;;) {
     if (threadIdx.x == 0) s_t = queue_pull(queue);
@@ -914,6 +909,7 @@ __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, 
     const PQG_G int64_t* doffs = gconst(job.dict_offs);
     for (int64_t i0 = v_lo; i0 < nn; i0 += 512) {
       const int64_t i = i0 + threadIdx.x;
+      const int64_t r_lo = s_prev;  // the round's first byte (read before any barrier moves it)
       int64_t e = 0, s0 = 0, from = 0;
       if (dict) {
         int64_t len = 0;
@@ -923,20 +919,39 @@ __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, 
           len = doffs[key + 1] - from;
         }
         int64_t tot;
-        const int64_t prev = s_prev;  // read before the scan's barriers: thread 0 moves it after
-        s0 = prev + block_excl_scan<512>(len, &tot, part);
+        s0 = r_lo + block_excl_scan<512>(len, &tot, part);
         e = s0 + len;
         if (threadIdx.x == 0) s_prev += tot;  // after the scan's last barrier
       } else {
         if (i < nn) {
           e = ends[i];
-          s0 = threadIdx.x ? ends[i - 1] : s_prev;
+          s0 = threadIdx.x ? ends[i - 1] : r_lo;
           from = dlba ? pg.cstart + s0 : s0 + 4 * (i + 1);
         }
         __syncthreads();  // every end of the round is read before any is rewritten
         if (i == (i0 + 512 < nn ? i0 + 511 : nn - 1)) s_prev = e;
       }
-      if (i < nn) {
+      __syncthreads();
+      const int64_t r_hi = s_prev;
+      const uintptr_t abs_lo = (uintptr_t)(chars + r_lo), abs_hi = (uintptr_t)(chars + r_hi);
+      const uintptr_t A0 = abs_lo & ~(uintptr_t)15;
+      if (abs_hi - A0 <= (uintptr_t)kCopyStage) {
+        if (i < nn) {
+          lds_copy(lds_ptr(stage) + ((uintptr_t)(chars + s0) - A0), src + from, e - s0);
+          ends[i] = base + e;
+        }
+        __syncthreads();
+        for (uintptr_t g = A0 + 16 * (uintptr_t)threadIdx.x; g < abs_hi; g += 16 * 512) {
+          const u32x4_t v = *(const PQG_L u32x4_t*)(lds_ptr(stage) + (g - A0));
+          if (g >= abs_lo && g + 16 <= abs_hi) {
+            stg16(g, make_uint4(v.x, v.y, v.z, v.w));
+          } else {
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            for (int b = 0; b < 16; b++)
+              if (g + b >= abs_lo && g + b < abs_hi) *(PQG_G uint8_t*)(g + b) = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+          }
+        }
+      } else if (i < nn) {
         copy_bytes(chars + s0, src + from, e - s0);
         ends[i] = base + e;
       }

@@ -7,7 +7,7 @@ from . import abi
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(HERE), "csrc", "libpqgpu.so")
 # diagnostics only: PQG_LIB may name the -DPQG_PROFILE build (libpqgpu_prof.so)
-LIB_PATH = os.environ.get("PQG_LIB", LIB_PATH)
+LIB_PATH = os.environ.get("PQG_LIB") or LIB_PATH
 
 _lib = None
 

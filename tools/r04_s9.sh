@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-4 session 9: snappy batches of up to 3 windows, far sources loaded
+# Round-4 session 9: block_walk over LDS chunks, k_str_copy through LDS; snappy batches of up to 3 windows, far sources loaded
 # ahead of the doubling: snappy parity, C3 / C4 / C5 bench lines, C4 phase counters.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_snappy.py tests/test_snappy_split.py tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest tests/test_snappy.py tests/test_snappy_split.py tests/test_gpu_parity.py tests/test_delta_strings.py -m gpu -x -q --timeout 120 --timeout-method thread \
   > gpurun_out/r04_s9_tests.txt 2>&1 || { tail -40 gpurun_out/r04_s9_tests.txt; exit 1; }
 tail -2 gpurun_out/r04_s9_tests.txt
 run() {  # name, config
