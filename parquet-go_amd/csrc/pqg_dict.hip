@@ -239,8 +239,9 @@ __device__ __forceinline__ int64_t dict_page(PieceShared& ps, const gcu8 sp, con
   while (kb < nb_all) {
     PQG_DT(ta);
     // ---- one round of loads: descriptors, run entries, payload window
-    uint4 q = make_uint4(0xffffffffu, 0u, 0u, 0u);
-    if (kb + lane < nb_all) q = ldg16((uintptr_t)(blks + kb + lane));
+    // (unconditional: a lane past the last block reads the last one, then
+    // takes the empty descriptor; a load under a branch is waited for inside it)
+    uint4 q = ldg16((uintptr_t)(blks + (kb + lane < nb_all ? kb + lane : nb_all - 1)));
     const uintptr_t ra = (uintptr_t)(runs + rcur);
     const uintptr_t ra_al = ra & ~(uintptr_t)15;
     const int rskew = (int)((ra - ra_al) >> 3);  // 0 or 1 entry before rcur
@@ -250,9 +251,9 @@ __device__ __forceinline__ int64_t dict_page(PieceShared& ps, const gcu8 sp, con
     const int64_t plo = pos - (int64_t)((pa + (uintptr_t)pos) & 15);  // 16-byte aligned address
     uint4 pg[kPG];
 #pragma unroll
-    for (int k = 0; k < kPG; k++) {
+    for (int k = 0; k < kPG; k++) {  // unconditional loads (see dbp_restage): zeroed when stored
       const int64_t at = plo + 16 * (int64_t)(lane + 64 * k);
-      pg[k] = at < n ? ldg16((uintptr_t)(sp + at)) : make_uint4(0u, 0u, 0u, 0u);
+      pg[k] = ldg16(at < n ? (uintptr_t)(sp + at) : (pa & ~(uintptr_t)15));
     }
 #pragma unroll
     for (int k = 0; k < kPRunGr; k++) sts16(lds_ptr(ps.runs) + 2 * (lane + 64 * k), rg[k]);
@@ -261,6 +262,7 @@ __device__ __forceinline__ int64_t dict_page(PieceShared& ps, const gcu8 sp, con
       const int64_t at = plo + 16 * (int64_t)(lane + 64 * k);
       sts16(lds_ptr(ps.stage) + 4 * (lane + 64 * k), mask_tail(pg[k], at, n));
     }
+    if (kb + lane >= nb_all) q = make_uint4(0xffffffffu, 0u, 0u, 0u);
     const uint32_t v0 = q.x, r0 = q.y, lo = q.z, nbytes = q.w & 0xffffu, nr = q.w >> 16;
     __builtin_amdgcn_wave_barrier();
     PQG_DT(tb);

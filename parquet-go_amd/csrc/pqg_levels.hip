@@ -567,11 +567,19 @@ struct LevelDecoder {
     wbase = at - mis;  // wraps below 0 for the first window of a misaligned stream: offsets are modular
     have = true;
     uint4 v[kLWin / 1024];
+    // granules holding a stream byte are mapped; bytes past n read as zero
+    // (Q5).  Every load is unconditional (a granule holding no stream byte
+    // reads the first one and is zeroed after all are issued: a load under a
+    // branch is waited for inside it).
 #pragma unroll
     for (int h = 0; h < kLWin / 1024; h++) {
       const int64_t g = (int64_t)at - mis + 1024 * h + 16 * lane;
-      // granules holding a stream byte are mapped; bytes past n read as zero (Q5)
-      v[h] = (g < (int64_t)n && g + 16 > 0) ? mask_tail(ldg16((uintptr_t)(p + g)), g, n) : make_uint4(0, 0, 0, 0);
+      v[h] = ldg16((g < (int64_t)n && g + 16 > 0) ? (uintptr_t)(p + g) : ((uintptr_t)p & ~(uintptr_t)15));
+    }
+#pragma unroll
+    for (int h = 0; h < kLWin / 1024; h++) {
+      const int64_t g = (int64_t)at - mis + 1024 * h + 16 * lane;
+      v[h] = (g < (int64_t)n && g + 16 > 0) ? mask_tail(v[h], g, n) : make_uint4(0, 0, 0, 0);
       if (g < 0 && g + 16 > 0) {  // bytes before the stream start: zero too (never read as data)
         uint32_t ww[4] = {v[h].x, v[h].y, v[h].z, v[h].w};
 #pragma unroll
@@ -1206,6 +1214,68 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
 __device__ void plan_parts(JobDev& job, int np, bool fail, const PageDev* pp, const HStream* streams,
                            const BlockDesc* blks, int* ctr, PartRec* parts, int64_t cap, int64_t* part);
 
+// The job's dictionary page and capacity checks (thread 0, after the notNull
+// scan): returns 1 when the job is out of capacity.
+__device__ int nn_job_tail(JobDev& job, PageDev* pages, uint8_t* scratch, int np, int64_t carry, bool fail0) {
+  int cap = fail0;
+  job.num_values = carry;
+  const int64_t vb = job.value_width > 0 ? carry * job.value_width : 0;
+  if (job.value_width > 0 && vb > job.value_cap) job.status = kCAPACITY, cap = 1;
+  job.values_bytes = vb;
+  // dictionary page (page_dict.go:30-64): PLAIN entries of the column type.
+  // The dictionary is published only when the page's read phase succeeds:
+  // the gather sinks bound keys by dict_count alone, so a short page must
+  // never be visible (the reference fails the chunk in readPages first).
+  if (job.dict_page >= 0 && job.dict_page < np) {
+    PageDev& dp = pages[job.page_base + job.dict_page];
+    if (dp.read_status == kOK) {
+      const uint8_t* blk =
+          dp.scratch_offset >= 0 ? scratch + job.scratch_base + dp.scratch_offset : job.data + dp.payload_offset;
+      const int64_t blen = dp.usize;
+      const int64_t cnt = dp.num_values;
+      const int w = job.value_width;
+      dp.block = blk;
+      dp.block_len = blen;
+      int st = kOK;
+      int flags = 0;
+      if (w > 0) {
+        if (job.type == 3) {  // INT96: a partial final entry is left nil, not an error (Q8)
+          const int64_t full = blen / 12, rem = blen % 12;
+          if (cnt > full + (rem > 0 ? 1 : 0)) st = kEOF;
+          else if (cnt == full + 1 && rem > 0) flags = 1;
+        } else if (cnt * w > blen) {
+          st = kEOF;
+        }
+      } else {
+        // u32-length entries (type_bytearray.go:24-45): k_str_dict walks them
+        // (every entry takes >= 4 bytes: a walk fails before entry blen/4 + 1)
+        flags = 2;
+        job.need_doffs = (cnt < blen / 4 ? cnt : blen / 4) + 2;
+        if (job.need_doffs > job.doffs_cap) job.status = kCAPACITY, cap = 1;
+      }
+      if (st == kOK) {
+        job.flags |= flags;
+        job.dict_data = blk;
+        job.dict_count = (flags & 2) ? 0 : cnt;  // byte arrays: published by k_str_dict after its walk
+        job.dict_len = blen;
+      } else {
+        dp.read_status = st;
+      }
+    }
+  }
+  return cap;
+}
+
+__device__ int64_t part_n(const PageDev& pg, const HStream* streams, int64_t* count, bool* hyb);
+__device__ void plan_split_pages(JobDev& job, const PageDev* pp, const HStream* streams, const BlockDesc* blks,
+                                 PartRec* parts, int64_t base, int nbig, const int* big, const int64_t* boff);
+__device__ void plan_parts_from(JobDev& job, int np, const PageDev* pp, const HStream* streams, const BlockDesc* blks,
+                                PartRec* parts, int64_t base);
+
+// Jobs of <= kNnFastSeg x 1024 pages: one read of each page's fields (kept in
+// registers), the notNull and part-count scans together, one write pass.
+constexpr int kNnFastSeg = 12;
+
 __global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch,
                                                   const HStream* streams, const BlockDesc* blks, int* ctr,
                                                   PartRec* parts, int64_t parts_cap) {
@@ -1214,6 +1284,120 @@ __global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, 
   JobDev& job = jobs[blockIdx.x];
   int np = job.num_pages < job.page_cap ? job.num_pages : job.page_cap;
   if (job.status == kCAPACITY) np = 0;
+  if (np <= kNnFastSeg * 1024) {
+    __shared__ int64_t s_base;
+    __shared__ int s_big[256];
+    __shared__ int64_t s_boff[256];
+    __shared__ int s_nbig;
+    const int seg = (np + 1023) / 1024;
+    const int s0 = (int)threadIdx.x * seg;
+    PageDev* pp = pages + job.page_base;
+    int32_t nnv[kNnFastSeg], kv[kNnFastSeg];
+    int8_t vm[kNnFastSeg];
+    int64_t nsum = 0, ksum = 0;
+    // the fields first, with unconditional loads (clamped page index: a
+    // guarded load would be waited for at its branch join), then the counts
+    int32_t f_type[kNnFastSeg], f_nn[kNnFastSeg], f_rs[kNnFastSeg], f_ds[kNnFastSeg], f_enc[kNnFastSeg];
+#pragma unroll
+    for (int j = 0; j < kNnFastSeg; j++) {
+      const int i = np > 0 ? (s0 + j < np ? s0 + j : np - 1) : 0;
+      const PageDev& pg = pp[i];
+      f_type[j] = pg.page_type;
+      f_nn[j] = pg.not_null;
+      f_rs[j] = pg.read_status;
+      f_ds[j] = pg.decode_status;
+      f_enc[j] = pg.encoding;
+      vm[j] = (int8_t)pg.vmode;
+    }
+#pragma unroll
+    for (int j = 0; j < kNnFastSeg; j++) {
+      nnv[j] = kv[j] = 0;
+      if (j < seg && s0 + j < np) {
+        const bool data = f_type[j] == 0 || f_type[j] == 3;
+        nnv[j] = data ? f_nn[j] : 0;
+        // part_n (below) from the fields: big hybrid pages read their stream
+        int32_t k = 0;
+        if (!data || vm[j] < 0) k = 0;
+        else if (f_rs[j] != kOK || f_ds[j] != kOK || vm[j] == 3) k = 1;
+        else if (vm[j] == 2 && f_enc[j] != 0 && f_enc[j] != 8) k = 1;
+        else if (f_nn[j] <= kSplitMin) k = 1;
+        else {
+          int64_t c;
+          bool h;
+          k = (int32_t)part_n(pp[s0 + j], streams, &c, &h);
+        }
+        kv[j] = k;
+      }
+      nsum += nnv[j];
+      ksum += kv[j];
+    }
+    int64_t carry, ktot;
+    int64_t run = block_excl_scan<1024>(nsum, &carry, part);
+    int64_t koff = block_excl_scan<1024>(ksum, &ktot, part);
+    const bool fail0 = job.status == kCAPACITY;
+    if (threadIdx.x == 0) {
+      int cap = nn_job_tail(job, pages, scratch, np, carry, fail0);
+      int64_t base = 0;
+      if (!cap) {
+        base = atomicAdd(ctr + kCtrItems, (int)ktot);
+        if (base + ktot > parts_cap) {
+          job.status = kCAPACITY;
+          cap = 1;
+        }
+      }
+      job.item_base = base;
+      job.n_items = cap ? 0 : (int32_t)ktot;
+      s_base = base;
+      s_cap = cap;
+      s_nbig = 0;
+    }
+    __syncthreads();
+    // value offsets (always: the later stages read them), then the parts
+#pragma unroll
+    for (int j = 0; j < kNnFastSeg; j++)
+      if (j < seg && s0 + j < np) {
+        pp[s0 + j].value_offset = run;
+        run += nnv[j];
+      }
+    if (s_cap) return;
+    const int64_t base = s_base;
+    bool more = false;
+#pragma unroll
+    for (int j = 0; j < kNnFastSeg; j++) {
+      if (j < seg && s0 + j < np) {
+        if (kv[j] == 1) {
+          PartRec r;
+          r.pidx = (int32_t)(job.page_base + s0 + j);
+          r.p = 0;
+          r.np = 1;
+          r.v0 = 0;
+          r.b0 = 0;
+          r.vmode = vm[j];
+          r.chars = r.cstart = r.prel = 0;
+          parts[base + koff] = r;
+        } else if (kv[j] > 1) {
+          const int slot = atomicAdd(&s_nbig, 1);
+          if (slot < 256) {
+            s_big[slot] = s0 + j;
+            s_boff[slot] = koff;
+          } else {
+            more = true;
+          }
+        }
+        koff += kv[j];
+      }
+    }
+    const bool any_more = __syncthreads_or(more);
+    const int nbig = s_nbig < 256 ? s_nbig : 256;
+    if (!any_more) {
+      plan_split_pages(job, pp, streams, blks, parts, base, nbig, s_big, s_boff);
+      return;
+    }
+    // more than 256 split pages: the general planner below writes every part again
+    __syncthreads();
+    plan_parts_from(job, np, pp, streams, blks, parts, base);
+    return;
+  }
   // each thread takes a contiguous segment of pages: its loads are
   // independent (one round trip per pass, not one per 1024 pages), one block
   // scan of the segment sums, then the offsets are written in a second pass
@@ -1235,54 +1419,7 @@ __global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, 
     run += nn_of(i);
   }
   const bool fail0 = job.status == kCAPACITY;
-  if (threadIdx.x == 0) {
-    s_cap = fail0;
-    job.num_values = carry;
-    const int64_t vb = job.value_width > 0 ? carry * job.value_width : 0;
-    if (job.value_width > 0 && vb > job.value_cap) job.status = kCAPACITY, s_cap = 1;
-    job.values_bytes = vb;
-    // dictionary page (page_dict.go:30-64): PLAIN entries of the column type.
-    // The dictionary is published only when the page's read phase succeeds:
-    // the gather sinks bound keys by dict_count alone, so a short page must
-    // never be visible (the reference fails the chunk in readPages first).
-    if (job.dict_page >= 0 && job.dict_page < np) {
-      PageDev& dp = pages[job.page_base + job.dict_page];
-      if (dp.read_status == kOK) {
-        const uint8_t* blk =
-            dp.scratch_offset >= 0 ? scratch + job.scratch_base + dp.scratch_offset : job.data + dp.payload_offset;
-        const int64_t blen = dp.usize;
-        const int64_t cnt = dp.num_values;
-        const int w = job.value_width;
-        dp.block = blk;
-        dp.block_len = blen;
-        int st = kOK;
-        int flags = 0;
-        if (w > 0) {
-          if (job.type == 3) {  // INT96: a partial final entry is left nil, not an error (Q8)
-            const int64_t full = blen / 12, rem = blen % 12;
-            if (cnt > full + (rem > 0 ? 1 : 0)) st = kEOF;
-            else if (cnt == full + 1 && rem > 0) flags = 1;
-          } else if (cnt * w > blen) {
-            st = kEOF;
-          }
-        } else {
-          // u32-length entries (type_bytearray.go:24-45): k_str_dict walks them
-          // (every entry takes >= 4 bytes: a walk fails before entry blen/4 + 1)
-          flags = 2;
-          job.need_doffs = (cnt < blen / 4 ? cnt : blen / 4) + 2;
-          if (job.need_doffs > job.doffs_cap) job.status = kCAPACITY, s_cap = 1;
-        }
-        if (st == kOK) {
-          job.flags |= flags;
-          job.dict_data = blk;
-          job.dict_count = (flags & 2) ? 0 : cnt;  // byte arrays: published by k_str_dict after its walk
-          job.dict_len = blen;
-        } else {
-          dp.read_status = st;
-        }
-      }
-    }
-  }
+  if (threadIdx.x == 0) s_cap = nn_job_tail(job, pages, scratch, np, carry, fail0);
   __syncthreads();
   // values-stage parts (below)
   plan_parts(job, np, s_cap != 0, pp, streams, blks, ctr, parts, parts_cap, part);
@@ -1313,27 +1450,73 @@ __device__ __forceinline__ int64_t part_count(const PageDev& pg, const HStream* 
   return 0;
 }
 
-__device__ __forceinline__ int64_t part_n(const PageDev& pg, const HStream* streams, int64_t* count, bool* hyb) {
+__device__ int64_t part_n(const PageDev& pg, const HStream* streams, int64_t* count, bool* hyb) {
   const int64_t c = part_count(pg, streams, hyb);
   *count = c;
   if (c < 0) return 0;
   return c > kSplitMin ? (c + kPart - 1) / kPart : 1;
 }
 
-// Called by k_nn_scan's block after its scan (the job's status in `fail`).
-// Each thread takes a contiguous segment of pages (independent loads, as in
-// the nn scan); one block scan gives every page its first slot.  Single-part
-// pages are written by their thread; split pages go through an LDS list, all
-// 1024 threads on each, in rounds of up to kBigList pages.
+// The parts of split pages (all threads of the block on each): big[q] is a
+// page of the job, boff[q] its first part's slot (relative to base).
+__device__ void plan_split_pages(JobDev& job, const PageDev* pp, const HStream* streams, const BlockDesc* blks,
+                                 PartRec* parts, int64_t base, int nbig, const int* big, const int64_t* boff) {
+  for (int q = 0; q < nbig; q++) {
+    const int pi = big[q];
+    const int64_t poff = boff[q];
+    int64_t cnt;
+    bool hyb;
+    const PageDev& pg = pp[pi];
+    const int64_t P = part_n(pg, streams, &cnt, &hyb);
+    PartRec r;
+    r.pidx = (int32_t)(job.page_base + pi);
+    r.np = (int32_t)P;
+    r.vmode = pg.vmode;
+    r.chars = r.cstart = r.prel = 0;
+    if (!hyb) {
+      for (int64_t p = threadIdx.x; p < P; p += blockDim.x) {
+        r.p = (int32_t)p;
+        r.v0 = (uint32_t)(p * kPart);
+        r.b0 = 0;
+        parts[base + poff + p] = r;
+      }
+    } else {
+      // part q starts at the first block whose first value is >= q kPart
+      // (blocks hold <= kHBlock <= kPart values, so every part but an
+      // empty tail one has a block start)
+      const HStream& S = streams[pg.hs_val];
+      const BlockDesc* B = blks + S.blk_base;
+      const int nb = S.n_blocks;
+      auto f = [&](int bi) -> int64_t {
+        if (bi < 0) return -1;
+        if (bi >= nb || (int64_t)B[bi].v0 >= cnt) return P;
+        return (int64_t)B[bi].v0 / kPart;
+      };
+      for (int bi = threadIdx.x; bi <= nb; bi += blockDim.x) {
+        const int64_t f1 = f(bi), f0 = f(bi - 1);
+        for (int64_t p = f0 + 1; p <= f1 && p < P; p++) {
+          r.p = (int32_t)p;
+          r.v0 = p == 0 ? 0u : (bi < nb && (int64_t)B[bi].v0 < cnt ? B[bi].v0 : (uint32_t)cnt);
+          r.b0 = bi;
+          parts[base + poff + p] = r;
+        }
+      }
+    }
+  }
+}
+
+// Every part of the job's pages from slot `base` on: each thread takes a
+// contiguous segment of pages (independent loads), one block scan gives every
+// page its first slot; single-part pages are written by their thread, split
+// pages go through an LDS list, all 1024 threads on each, in rounds of up to
+// kBigList pages.
 constexpr int kBigList = 256;
-__device__ void plan_parts(JobDev& job, int np, bool fail, const PageDev* pp, const HStream* streams,
-                           const BlockDesc* blks, int* ctr, PartRec* parts, int64_t cap, int64_t* part) {
-  __shared__ int64_t s_base;
-  __shared__ int s_fail;
+__device__ void plan_parts_from(JobDev& job, int np, const PageDev* pp, const HStream* streams, const BlockDesc* blks,
+                                PartRec* parts, int64_t base) {
+  __shared__ int64_t part2[17];
   __shared__ int s_big[kBigList];
   __shared__ int64_t s_boff[kBigList];
   __shared__ int s_nbig;
-  if (fail) np = 0;
   const int seg = (np + 1023) / 1024;
   const int s0 = (int)threadIdx.x * seg, s1 = s0 + seg < np ? s0 + seg : np;
   int64_t sum = 0;
@@ -1343,18 +1526,7 @@ __device__ void plan_parts(JobDev& job, int np, bool fail, const PageDev* pp, co
     sum += part_n(pp[i], streams, &c, &h);
   }
   int64_t tot;
-  int64_t off = block_excl_scan<1024>(sum, &tot, part);
-  if (threadIdx.x == 0) {
-    const int64_t base = fail ? 0 : atomicAdd(ctr + kCtrItems, (int)tot);
-    s_fail = fail || base + tot > cap;
-    if (!fail && s_fail) job.status = kCAPACITY;
-    job.item_base = base;
-    job.n_items = s_fail ? 0 : (int32_t)tot;
-    s_base = base;
-  }
-  __syncthreads();
-  if (s_fail) return;
-  const int64_t base = s_base;
+  int64_t off = block_excl_scan<1024>(sum, &tot, part2);
   int cur = s0;
   for (;;) {
     if (threadIdx.x == 0) s_nbig = 0;
@@ -1384,51 +1556,39 @@ __device__ void plan_parts(JobDev& job, int np, bool fail, const PageDev* pp, co
       off += k;
     }
     __syncthreads();
-    const int nbig = s_nbig < kBigList ? s_nbig : kBigList;
-    for (int q = 0; q < nbig; q++) {
-      const int pi = s_big[q];
-      const int64_t poff = s_boff[q];
-      int64_t cnt;
-      bool hyb;
-      const PageDev& pg = pp[pi];
-      const int64_t P = part_n(pg, streams, &cnt, &hyb);
-      PartRec r;
-      r.pidx = (int32_t)(job.page_base + pi);
-      r.np = (int32_t)P;
-      r.vmode = pg.vmode;
-      r.chars = r.cstart = r.prel = 0;
-      if (!hyb) {
-        for (int64_t p = threadIdx.x; p < P; p += 1024) {
-          r.p = (int32_t)p;
-          r.v0 = (uint32_t)(p * kPart);
-          r.b0 = 0;
-          parts[base + poff + p] = r;
-        }
-      } else {
-        // part q starts at the first block whose first value is >= q kPart
-        // (blocks hold <= kHBlock <= kPart values, so every part but an
-        // empty tail one has a block start)
-        const HStream& S = streams[pg.hs_val];
-        const BlockDesc* B = blks + S.blk_base;
-        const int nb = S.n_blocks;
-        auto f = [&](int bi) -> int64_t {
-          if (bi < 0) return -1;
-          if (bi >= nb || (int64_t)B[bi].v0 >= cnt) return P;
-          return (int64_t)B[bi].v0 / kPart;
-        };
-        for (int bi = threadIdx.x; bi <= nb; bi += 1024) {
-          const int64_t f1 = f(bi), f0 = f(bi - 1);
-          for (int64_t p = f0 + 1; p <= f1 && p < P; p++) {
-            r.p = (int32_t)p;
-            r.v0 = p == 0 ? 0u : (bi < nb && (int64_t)B[bi].v0 < cnt ? B[bi].v0 : (uint32_t)cnt);
-            r.b0 = bi;
-            parts[base + poff + p] = r;
-          }
-        }
-      }
-    }
+    plan_split_pages(job, pp, streams, blks, parts, base, s_nbig < kBigList ? s_nbig : kBigList, s_big, s_boff);
     if (!__syncthreads_or(cur < s1)) break;
   }
+}
+
+// Called by k_nn_scan's block after its scan (the job's status in `fail`):
+// the job's slot range, then its parts.
+__device__ void plan_parts(JobDev& job, int np, bool fail, const PageDev* pp, const HStream* streams,
+                           const BlockDesc* blks, int* ctr, PartRec* parts, int64_t cap, int64_t* part) {
+  __shared__ int64_t s_base;
+  __shared__ int s_fail;
+  if (fail) np = 0;
+  const int seg = (np + 1023) / 1024;
+  const int s0 = (int)threadIdx.x * seg, s1 = s0 + seg < np ? s0 + seg : np;
+  int64_t sum = 0;
+  for (int i = s0; i < s1; i++) {
+    int64_t c;
+    bool h;
+    sum += part_n(pp[i], streams, &c, &h);
+  }
+  int64_t tot;
+  block_excl_scan<1024>(sum, &tot, part);
+  if (threadIdx.x == 0) {
+    const int64_t base = fail ? 0 : atomicAdd(ctr + kCtrItems, (int)tot);
+    s_fail = fail || base + tot > cap;
+    if (!fail && s_fail) job.status = kCAPACITY;
+    job.item_base = base;
+    job.n_items = s_fail ? 0 : (int32_t)tot;
+    s_base = base;
+  }
+  __syncthreads();
+  if (s_fail) return;
+  plan_parts_from(job, np, pp, streams, blks, parts, s_base);
 }
 
 }  // namespace pqg

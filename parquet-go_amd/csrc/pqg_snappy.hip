@@ -58,7 +58,8 @@ constexpr int kSnWin = 4096;      // compressed-stream window (LDS)
 constexpr int kSnWinNeed = 2048;  // window bytes wanted ahead of the first tag
 constexpr int kSpan = 1024;       // output bytes a batch covers: 64 lanes x one 16-byte granule
 #ifndef PQG_SNAPPY_RING
-#define PQG_SNAPPY_RING 8192
+#define PQG_SNAPPY_RING 4096  // 4 KiB + 12 KiB of tables: 12 waves per CU (8 KiB: 9; r04 session 10: C4 snappy
+                              // 11.95 -> 10.00 ms, C3 1.20 -> 0.93 ms with <= 168 VGPRs)
 #endif
 constexpr int kRing = PQG_SNAPPY_RING;  // output history kept in LDS (a power of two)
 // flush granularity (a wave's stores are waited for at the next loop head);
@@ -69,7 +70,7 @@ static_assert((kRing & (kRing - 1)) == 0 && kRing >= 4096, "ring: a power of two
 constexpr int kLongPiece = kRing >= 8192 ? 4096 : 1024;  // literal piece read from HBM
 constexpr int kWinLit = 1024;     // literals up to this many bytes (after the granule prefix) move from the window
 #ifndef PQG_SNAPPY_WPE
-#define PQG_SNAPPY_WPE 1  // waves per EU the decoder is compiled for (3: <= 168 VGPRs)
+#define PQG_SNAPPY_WPE 3  // waves per EU the decoder is compiled for (3: <= 168 VGPRs, no spills)
 #endif
 #ifndef PQG_SNAPPY_SERIAL_CHAIN
 #define PQG_SNAPPY_SERIAL_CHAIN 0
@@ -311,7 +312,9 @@ struct SnapBlock {
 #pragma unroll
     for (int h = 0; h < kSnWin / 1024; h++) {
       const int64_t g = in_base + 1024 * h + 16 * lane;
-      // a granule holding a byte of [0, slen) is mapped
+      // a granule holding a byte of [0, slen) is mapped (these loads stay
+      // guarded: unconditional ones push the decoder past its 168 VGPRs; the
+      // refills are ~1 % of its time, r04 session 10 counters)
       v[h] = (g < slen && g + 16 > 0) ? ldg16((uintptr_t)(src + g)) : make_uint4(0, 0, 0, 0);
     }
     __builtin_amdgcn_wave_barrier();
@@ -1032,14 +1035,18 @@ __global__ void __launch_bounds__(64) k_snap_seg(const JobDev* jobs, const PageD
     // byte are mapped; the others read as zero)
     const int64_t st_lo = b - (int64_t)(((uintptr_t)(src + b)) & 15);
     uint4 v[kStG];
+    const uintptr_t safe = (uintptr_t)src & ~(uintptr_t)15;  // unconditional loads (see SnapBlock::fill)
 #pragma unroll
     for (int k = 0; k < kStG; k++) {
       const int64_t o = st_lo + 16 * (int64_t)(lane + 64 * k);
-      v[k] = (o < L.clen && o + 16 > 0) ? ldg16((uintptr_t)(src + o)) : make_uint4(0u, 0u, 0u, 0u);
+      v[k] = ldg16((o < L.clen && o + 16 > 0) ? (uintptr_t)(src + o) : safe);
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int k = 0; k < kStG; k++) sts16(lds_ptr(st) + 16 * (lane + 64 * k), v[k]);
+    for (int k = 0; k < kStG; k++) {
+      const int64_t o = st_lo + 16 * (int64_t)(lane + 64 * k);
+      sts16(lds_ptr(st) + 16 * (lane + 64 * k), (o < L.clen && o + 16 > 0) ? v[k] : make_uint4(0u, 0u, 0u, 0u));
+    }
     __builtin_amdgcn_wave_barrier();
     int64_t x = b + lane;
     uint32_t acc = 0;

@@ -69,7 +69,8 @@ int prof_read_strings(unsigned long long* out) {
 // whether the chunk takes the serial walk (for text-like records: never).
 // ---------------------------------------------------------------------------
 constexpr int kWalkT = 512;
-constexpr int kPwSeg = 64;                  // bytes per thread segment
+constexpr int kPwSeg = 68;                  // bytes per thread segment (17 dwords: the lanes' reads
+                                            // at the same offset of their segments hit distinct banks)
 constexpr int kPwChunk = kWalkT * kPwSeg;   // bytes per chunk (LDS)
 constexpr int kPwRec = kPwSeg / 4;          // records a segment can hold (>= 4 bytes each)
 constexpr int kPwAhead = 4096;              // staged past the chunk: the guesses' chain checks
@@ -109,19 +110,25 @@ __device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out
   }
   const uintptr_t pend = (uintptr_t)(p + n);
   // granule k of the chunk from c0 (aligned start): mapped when it holds a stream byte
+  // unconditional loads (a guarded load is waited for at its branch join,
+  // which would make this prefetch synchronous): granules past the stream's
+  // last one re-read that one; their bytes are never interpreted (every
+  // length read checks n first)
+  const uintptr_t lastg = (pend - 1) & ~(uintptr_t)15;
   auto load_chunk = [&](uint32_t c0, uint4 (&v)[kPwG]) {
     const uintptr_t A = (uintptr_t)(p + c0) & ~(uintptr_t)15;
 #pragma unroll
     for (int k = 0; k < kPwG; k++) {
       const uintptr_t g = A + 16 * (uintptr_t)(t + kWalkT * k);
-      v[k] = (g < pend && g - A < (uintptr_t)kPwStage) ? ldg16(g) : make_uint4(0u, 0u, 0u, 0u);
+      v[k] = ldg16(g < lastg ? g : lastg);
     }
   };
   uint4 nx[kPwG];
-  if (count > 0) load_chunk(0, nx);
+  if (count > 0 && n > 0) load_chunk(0, nx);
   __syncthreads();
   for (uint32_t c0 = 0; count > 0 && c0 < n; c0 += kPwChunk) {
     const uint32_t c1 = n - c0 > (uint32_t)kPwChunk ? c0 + kPwChunk : n;
+    PQG_T(tq0);
     const uint32_t cur = sh.cur, idx0 = sh.idx;
     if (idx0 >= count) break;
     if (cur >= c1) {  // a record spans the chunk
@@ -134,6 +141,8 @@ __device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out
     __syncthreads();
     if (c1 < n) load_chunk(c1, nx);
     PQG_ACC0(21, 1);
+    PQG_T(tq1);
+    PQG_ACC0(16, tq1 - tq0);
     const uint32_t off0 = (uint32_t)(((uintptr_t)(p + c0)) & 15);  // buf index of stream position c0
     const PQG_L uint8_t* B = lds_ptr(sh.buf);
     auto len_at = [&](uint32_t q) { return lds_u32(B, q - c0 + off0); };  // q + 4 <= c1 + kPwAhead + 48
@@ -153,12 +162,47 @@ __device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out
         // wins (the true entry starts the longest run: a false start two or
         // three bytes before a record may jump onto the true chain, but only
         // after leaving the segment), then the nearest exit
+        // 1. screen: the positions whose own length is valid, from two aligned
+        //    LDS dwords per four positions (no dependent reads), as a bit mask
+        uint32_t m0 = 0, m1 = 0, m2 = 0;  // bit i: position lo + i (i < kPwSeg <= 96)
+        const uint32_t b_lo = (lo - c0 + off0) & ~3u, b_hi = hi - c0 + off0;
+        for (uint32_t b4 = b_lo; b4 < b_hi; b4 += 4) {
+          const uint32_t w0 = *(const PQG_L uint32_t*)(B + b4), w1 = *(const PQG_L uint32_t*)(B + b4 + 4);
+#pragma unroll
+          for (int kq = 0; kq < 4; kq++) {
+            const uint32_t q = c0 - off0 + b4 + kq;
+            const uint32_t l0 = kq ? __builtin_amdgcn_alignbit(w1, w0, 8 * kq) : w0;
+            const bool ok = q >= lo && q < hi && n - q >= 4 && (int32_t)l0 >= 0 && n - q - 4 >= l0;
+            const uint32_t i = q - lo;  // < 96 when ok
+            const uint32_t bit = ok ? 1u << (i & 31) : 0u;
+            m0 |= i < 32 ? bit : 0u;
+            m1 |= i >= 32 && i < 64 ? bit : 0u;
+            m2 |= i >= 64 ? bit : 0u;
+          }
+        }
+        // 2. the candidates in order (a wave loops as often as its lane with
+        //    the most candidates): every record up to hi and two more after
+        //    them valid (inside the staged bytes, or to the end of the
+        //    stream); the one with the most records in the segment wins (the
+        //    true entry starts the longest run: a false start two or three
+        //    bytes before a record may jump onto the true chain, but only
+        //    after leaving the segment), then the nearest exit
         uint32_t best_k = 0, best_x = 0xffffffffu;
-        for (uint32_t q = lo; q < hi; q++) {
-          uint32_t r = q, kk = 0;
-          bool ok = true;
+        while (m0 | m1 | m2) {
+          const uint32_t i = m0 ? __builtin_ctz(m0) : m1 ? 32 + __builtin_ctz(m1) : 64 + __builtin_ctz(m2);
+          if (i < 32) m0 &= m0 - 1;
+          else if (i < 64) m1 &= m1 - 1;
+          else m2 &= m2 - 1;
+          const uint32_t q = lo + i;
+          {
+          uint32_t r = q, kk = 0, x = 0;  // x: this candidate's exit (its first record start >= hi)
+          bool ok = true, xs = false;
           int extra = 0;
           while (ok && extra < 2) {
+            if (!xs && r >= hi) {
+              x = r;
+              xs = true;
+            }
             if (r == n) break;
             if (r >= c1 + kPwAhead) break;  // leaves the staged bytes: no further check
             if (n - r < 4) { ok = false; break; }
@@ -169,13 +213,13 @@ __device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out
             r += 4 + l;
           }
           if (!ok) continue;
-          uint32_t x = q;  // this candidate's exit
-          while (x < hi) x += 4 + len_at(x);  // (validated above)
+          if (!xs) x = r;  // (r >= hi here: n and the staged end lie at or past hi)
           if (kk > best_k || (kk == best_k && x < best_x)) {
             best_k = kk;
             best_x = x;
             g = q;
             has = true;
+          }
           }
         }
       }
@@ -195,6 +239,8 @@ __device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out
       }
     }
     // ---- check every guess at once: entry == exit of the nearest segment before with records
+    PQG_T(tq2);
+    PQG_ACC0(17, tq2 - tq1);
     sh.X[t] = x;
     int key = has ? t + 1 : 0;  // inclusive max-scan of the segments with records
 #pragma unroll
@@ -252,6 +298,8 @@ __device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out
       sh.status = st;
     }
     __syncthreads();
+    PQG_T(tq3);
+    PQG_ACC0(18, tq3 - tq2);
     if (sh.status != kOK) return sh.status;
   }
   __syncthreads();

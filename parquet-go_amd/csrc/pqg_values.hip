@@ -198,15 +198,19 @@ __device__ __forceinline__ void dbp_restage(gcu8 s, int64_t n, PQG_L uint8_t* st
   const int lane = lane_id();
   st_lo = at - (int64_t)(((uintptr_t)(s + at)) & 15);
   uint4 g[kDStage / 1024];
+  // every load unconditional (a granule holding no stream byte reads the
+  // stream's first one and is zeroed after all are issued: a load under a
+  // branch is waited for inside it)
+  const uintptr_t safe = (uintptr_t)s & ~(uintptr_t)15;
 #pragma unroll
   for (int k = 0; k < kDStage / 1024; k++) {
     const int64_t o = st_lo + 16 * (int64_t)(lane + 64 * k);
-    g[k] = (o < n && o + 16 > 0) ? ldg16((uintptr_t)(s + o)) : make_uint4(0u, 0u, 0u, 0u);
+    g[k] = ldg16((o < n && o + 16 > 0) ? (uintptr_t)(s + o) : safe);
   }
 #pragma unroll
   for (int k = 0; k < kDStage / 1024; k++) {
     const int64_t o = st_lo + 16 * (int64_t)(lane + 64 * k);
-    sts16(stb + 16 * (lane + 64 * k), mask_tail(g[k], o, n));
+    sts16(stb + 16 * (lane + 64 * k), (o < n && o + 16 > 0) ? mask_tail(g[k], o, n) : make_uint4(0u, 0u, 0u, 0u));
   }
   st_hi = st_lo + kDStage;
   __builtin_amdgcn_wave_barrier();
