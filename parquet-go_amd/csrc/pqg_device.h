@@ -35,6 +35,21 @@ __device__ __forceinline__ void stg16(uintptr_t a, uint4 x) {
   const u32x4_t v = {x.x, x.y, x.z, x.w};
   *(PQG_G u32x4_t*)a = v;
 }
+// Decoded-output stores: the outputs are not read again by the pipeline, so
+// they are stored non-temporally (PQG_NT_OUT, default on: the L2 keeps what
+// later kernels re-read -- dictionaries, run tables, pages; C2 3.31 -> 3.25 ms
+// with k_dict4's stores, r04 session 15).
+#ifndef PQG_NT_OUT
+#define PQG_NT_OUT 1
+#endif
+__device__ __forceinline__ void stg16o(uintptr_t a, uint4 x) {
+#if PQG_NT_OUT
+  const u32x4_t v = {x.x, x.y, x.z, x.w};
+  __builtin_nontemporal_store(v, (PQG_G u32x4_t*)a);
+#else
+  stg16(a, x);
+#endif
+}
 __device__ __forceinline__ void stg8(uintptr_t a, uint32_t lo, uint32_t hi) {
   const u32x2_t v = {lo, hi};
   *(PQG_G u32x2_t*)a = v;
@@ -189,7 +204,7 @@ __device__ __forceinline__ void store_run_aligned(uintptr_t base, const uint32_t
         const u32x4_t v = {w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]};
         __builtin_nontemporal_store(v, (PQG_G u32x4_t*)(o + 16 * g));
       } else {
-        stg16(o + 16 * g, make_uint4(w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]));
+        stg16o(o + 16 * g, make_uint4(w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]));
       }
     }
   } else {
@@ -237,7 +252,7 @@ __device__ __forceinline__ void wave_copy_body(PQG_G uint8_t* db, uintptr_t sbas
       o.y = __builtin_amdgcn_alignbit(w[Q + 2], w[Q + 1], r);
       o.z = __builtin_amdgcn_alignbit(w[Q + 3], w[Q + 2], r);
       o.w = __builtin_amdgcn_alignbit(w[Q + 4 < 8 ? Q + 4 : 7], w[Q + 3], r);
-      stg16((uintptr_t)(db + g), o);
+      stg16o((uintptr_t)(db + g), o);
     }
   }
 }

@@ -111,6 +111,19 @@ struct DProf {
 #define PQG_DT(v) const uint64_t v = 0
 #endif
 
+// Output stores: non-temporal (streaming), so that the output stream does not
+// evict the dictionary's L2 lines (b = 20: 4 MiB, the size of one XCD's L2).
+#ifndef PQG_DICT_NT
+#define PQG_DICT_NT PQG_NT_OUT
+#endif
+__device__ __forceinline__ void dict_store(PQG_G uint32_t* p, uint32_t v) {
+#if PQG_DICT_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 // One block of a piece, wave-uniform fields (read from lanes of the descriptor registers).
 struct PBlock {
   uint32_t v0, v1;   // values [v0, v1)
@@ -149,7 +162,7 @@ __device__ __forceinline__ void block_out(PieceShared& ps, const PBlock& B, uint
       if (src >= dcount) bad = (int64_t)B.v0 < bad ? (int64_t)B.v0 : bad;
 #pragma unroll
       for (int q = 0; q < 8; q++)
-        if ((uint32_t)(lane + 64 * q) < nv) out[lane + 64 * q] = x;
+        if ((uint32_t)(lane + 64 * q) < nv) dict_store(out + lane + 64 * q, x);
       return;
     }
     const uint32_t rb0 = (uint32_t)((int64_t)src * 8 - plo8) + (B.v0 + (uint32_t)lane - (st & ~kRunBP)) * (uint32_t)w;
@@ -208,7 +221,7 @@ __device__ __forceinline__ void block_out(PieceShared& ps, const PBlock& B, uint
   for (int q = 0; q < 8; q++) val[q] = dict((uint32_t)(lane + 64 * q) < nv ? key[q] : 0u);
 #pragma unroll
   for (int q = 0; q < 8; q++)
-    if ((uint32_t)(lane + 64 * q) < nv) out[lane + 64 * q] = val[q];
+    if ((uint32_t)(lane + 64 * q) < nv) dict_store(out + lane + 64 * q, val[q]);
 }
 
 // Decode one page (or a part of a big page): keys piece by piece, looked up
@@ -421,7 +434,7 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, kDWaves * 64), amd
 #pragma unroll
         for (int k = 0; k < kDictLdsEntries / (kDWaves * 64); k++) {
           const int i = (int)threadIdx.x + k * kDWaves * 64;
-          rr[k] = i < dc ? src[i] : 0u;
+          rr[k] = src[i < dc ? i : 0];  // unconditional (a load under a branch is waited for inside it)
         }
 #pragma unroll
         for (int k = 0; k < kDictLdsEntries / (kDWaves * 64); k++) {

@@ -393,7 +393,7 @@ __global__ void __launch_bounds__(64) k_level_long(PageDev* pages, const int* ct
 #pragma unroll
       for (int k = 0; k < 4; k++) wv[k] = v[4 * k] | v[4 * k + 1] << 8 | v[4 * k + 2] << 16 | v[4 * k + 3] << 24;
       if (i0 >= (int64_t)pc.v0 && i0 + 16 <= (int64_t)pc.v1) {
-        stg16(a, make_uint4(wv[0], wv[1], wv[2], wv[3]));
+        stg16o(a, make_uint4(wv[0], wv[1], wv[2], wv[3]));
 #pragma unroll
         for (int k = 0; k < 16; k++) nn += v[k] == (uint32_t)L.maxl;
       } else {
@@ -640,7 +640,7 @@ struct LevelDecoder {
     for (int k = 0; k < 4; k++) wv[k] = val[4 * k] | val[4 * k + 1] << 8 | val[4 * k + 2] << 16 | val[4 * k + 3] << 24;
     const int i0 = 16 * lane;
     if (i0 >= pre && i0 + 16 <= end) {
-      stg16(a0 + i0, make_uint4(wv[0], wv[1], wv[2], wv[3]));
+      stg16o(a0 + i0, make_uint4(wv[0], wv[1], wv[2], wv[3]));
 #pragma unroll
       for (int k = 0; k < 16; k++) nn += val[k] == maxl;
     } else if (i0 + 16 > pre && i0 < end) {
@@ -701,7 +701,7 @@ struct LevelDecoder {
     constexpr bool kStore = true;
 #endif
     if (i0 >= pre && i0 + 16 <= end) {
-      if (kStore) stg16(a0 + i0, make_uint4(wv[0], wv[1], wv[2], wv[3]));
+      if (kStore) stg16o(a0 + i0, make_uint4(wv[0], wv[1], wv[2], wv[3]));
       if (maxl == 1) nn += __builtin_popcount(b16);
     } else if (i0 + 16 > pre && i0 < end) {
       uint32_t vm = 0;

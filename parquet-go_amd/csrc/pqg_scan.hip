@@ -211,11 +211,13 @@ __device__ __forceinline__ void parse_candidate(const JobDev& job, int64_t p, Sk
     const uintptr_t a0 = (uintptr_t)(job.data + p) & ~(uintptr_t)15;
     const int64_t lo = p - (int64_t)((uintptr_t)(job.data + p) - a0);  // chunk offset of the first granule
     uint4 g[kCandWin];
+    // a granule holding a byte < n is mapped; the others read the first one
+    // and are zeroed after every load is issued (a load under a branch is
+    // waited for inside it)
 #pragma unroll
-    for (int k = 0; k < kCandWin; k++)  // a granule holding a byte < n is mapped
-      g[k] = lo + 16 * k < job.data_len ? ldg16(a0 + 16 * k) : make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < kCandWin; k++) g[k] = ldg16(lo + 16 * k < job.data_len ? a0 + 16 * k : a0);
 #pragma unroll
-    for (int k = 0; k < kCandWin; k++) sts16(win + 16 * k, g[k]);
+    for (int k = 0; k < kCandWin; k++) sts16(win + 16 * k, lo + 16 * k < job.data_len ? g[k] : make_uint4(0, 0, 0, 0));
     c.src.win = win;
     c.src.wlo = lo;
     c.src.whi = lo + 16 * kCandWin < job.data_len ? lo + 16 * kCandWin : job.data_len;
@@ -311,8 +313,10 @@ __global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, const int* til
   for (int it = 0; it < kG; it++) {
     const uintptr_t a = a0 + (int64_t)tid * 16 + (int64_t)it * 256 * 16;
     const int64_t p0 = (int64_t)(a - (uintptr_t)base);
-    // a granule holding a position < t1 <= data_len is mapped
-    vv[it] = p0 < t1 ? ldg16(a) : make_uint4(0, 0, 0, 0);
+    // a granule holding a position < t1 <= data_len is mapped; the others
+    // re-read the tile's first one (unconditional: a load under a branch is
+    // waited for inside it) and are never examined
+    vv[it] = ldg16(p0 < t1 ? a : a0);
   }
 #pragma unroll
   for (int it = 0; it < kG; it++) {

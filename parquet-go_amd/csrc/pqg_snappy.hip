@@ -72,6 +72,9 @@ constexpr int kWinLit = 1024;     // literals up to this many bytes (after the g
 #ifndef PQG_SNAPPY_WPE
 #define PQG_SNAPPY_WPE 3  // waves per EU the decoder is compiled for (3: <= 168 VGPRs, no spills)
 #endif
+#ifndef PQG_SNAPPY_LL_UNCOND
+#define PQG_SNAPPY_LL_UNCOND 1  // long literals: unconditional piece loads (36 B of spills at 168 VGPRs)
+#endif
 #ifndef PQG_SNAPPY_SERIAL_CHAIN
 #define PQG_SNAPPY_SERIAL_CHAIN 0
 #endif
@@ -340,7 +343,7 @@ struct SnapBlock {
 
   // A literal too long for one batch (or whose bytes leave the window):
   // pieces of up to kLongPiece bytes straight from the compressed block.
-  __device__ void long_literal(int64_t at, int64_t len) {
+  __device__ __attribute__((noinline)) void long_literal(int64_t at, int64_t len) {
     const int lane = lane_id();
     constexpr int NG = kLongPiece / 1024;  // granules per lane
     while (len > 0) {
@@ -350,6 +353,7 @@ struct SnapBlock {
       const int64_t lim = pre + piece;  // piece bytes are [pre, lim) of the granules from a0
       uint4 x[NG], y[NG];
       uint32_t r[NG];
+      bool nx[NG], ny[NG];
 #pragma unroll
       for (int j = 0; j < NG; j++) {
         const int64_t i0 = 1024 * j + 16 * lane;  // granule's first byte (relative to a0)
@@ -360,9 +364,26 @@ struct SnapBlock {
         // load an aligned granule only if it holds a byte of the piece
         const int64_t lo = at + (i0 > pre ? i0 - pre : 0), hi = at + (i0 + 16 < lim ? i0 + 16 : lim) - pre;
         const bool need = i0 < lim && i0 + 16 > pre;
-        x[j] = (need && gb0 + 16 > lo) ? ldg16(sa & ~(uintptr_t)15) : make_uint4(0, 0, 0, 0);
-        y[j] = (need && r[j] != 0 && gb0 + 16 < hi) ? ldg16((sa & ~(uintptr_t)15) + 16) : make_uint4(0, 0, 0, 0);
+        // unconditional loads (a load under a branch is waited for inside it):
+        // a granule not needed re-reads the literal's first one, zeroed below
+        nx[j] = need && gb0 + 16 > lo;
+        ny[j] = need && r[j] != 0 && gb0 + 16 < hi;
+#if PQG_SNAPPY_LL_UNCOND
+        const uintptr_t safe = (uintptr_t)(src + at) & ~(uintptr_t)15;
+        x[j] = ldg16(nx[j] ? sa & ~(uintptr_t)15 : safe);
+        y[j] = ldg16(ny[j] ? (sa & ~(uintptr_t)15) + 16 : safe);
+#else
+        x[j] = nx[j] ? ldg16(sa & ~(uintptr_t)15) : make_uint4(0, 0, 0, 0);
+        y[j] = ny[j] ? ldg16((sa & ~(uintptr_t)15) + 16) : make_uint4(0, 0, 0, 0);
+#endif
       }
+#if PQG_SNAPPY_LL_UNCOND
+#pragma unroll
+      for (int j = 0; j < NG; j++) {
+        if (!nx[j]) x[j] = make_uint4(0, 0, 0, 0);
+        if (!ny[j]) y[j] = make_uint4(0, 0, 0, 0);
+      }
+#endif
 #pragma unroll
       for (int j = 0; j < NG; j++) {
         const int64_t i0 = 1024 * j + 16 * lane;

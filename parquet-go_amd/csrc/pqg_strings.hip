@@ -308,9 +308,231 @@ __device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out
   return kOK;
 }
 
+// ---------------------------------------------------------------------------
+// Dictionary pages (k_str_dict: one block per chunk, so the whole page's
+// parallelism must come from one block): the page is cut into 512 segments
+// walked at once through 64-byte register windows from global memory (a
+// two-guess start per segment, thread 0 chains the guesses, a second pass
+// writes), instead of block_walk's 32 KiB chunks one after another.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t pick4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+  return (k & 2) ? ((k & 1) ? d : c) : ((k & 1) ? b : a);
+}
+
+// Walk records from `pos` while pos < stop and fewer than `limit` records are
+// done.  Returns the records walked; *end = the position after them, *fail = 1
+// when the record at *end is not valid (length negative or past n, or fewer
+// than 4 bytes left).  sink(k, pos_after) sees record k of the walk.
+template <class F>
+__device__ __forceinline__ uint32_t seg_walk(gcu8 p, uint32_t n, uint32_t pos, uint32_t stop, uint32_t limit,
+                                             uint32_t* end, int* fail, F&& sink) {
+  uintptr_t wb = 0;
+  uint4 g0 = make_uint4(0, 0, 0, 0), g1 = g0, g2 = g0, g3 = g0;
+  const uintptr_t pend = (uintptr_t)(p + n);
+  uint32_t k = 0;
+  *fail = 0;
+  while (pos < stop && k < limit) {
+    if (n - pos < 4) { *fail = 1; break; }
+    const uintptr_t a = (uintptr_t)(p + pos);
+    if (a < wb || a + 4 > wb + 64) {
+      wb = a & ~(uintptr_t)15;
+      // four loads issued together, unconditionally (a guarded load would be
+      // waited for at its branch join): granules past the stream's last one
+      // re-read that one, their bytes are never used
+      const uintptr_t lastg = (pend - 1) & ~(uintptr_t)15;
+      g0 = ldg16(wb);
+      g1 = ldg16(wb + 16 < lastg ? wb + 16 : lastg);
+      g2 = ldg16(wb + 32 < lastg ? wb + 32 : lastg);
+      g3 = ldg16(wb + 48 < lastg ? wb + 48 : lastg);
+    }
+    const uint32_t off = (uint32_t)(a - wb), d = off >> 2, e = d + 1 < 16 ? d + 1 : 15;
+    const uint32_t lo = pick4(pick4(g0.x, g0.y, g0.z, g0.w, d), pick4(g1.x, g1.y, g1.z, g1.w, d),
+                              pick4(g2.x, g2.y, g2.z, g2.w, d), pick4(g3.x, g3.y, g3.z, g3.w, d), d >> 2);
+    const uint32_t hi = pick4(pick4(g0.x, g0.y, g0.z, g0.w, e), pick4(g1.x, g1.y, g1.z, g1.w, e),
+                              pick4(g2.x, g2.y, g2.z, g2.w, e), pick4(g3.x, g3.y, g3.z, g3.w, e), e >> 2);
+    const uint32_t l = __builtin_amdgcn_alignbit(hi, lo, (off & 3) * 8);
+    if ((int32_t)l < 0 || n - pos - 4 < l) { *fail = 1; break; }
+    pos += 4 + l;
+    sink(k, pos);
+    k++;
+  }
+  *end = pos;
+  return k;
+}
+
+struct BlockWalkSharedG {
+  uint32_t start[kWalkT];  // pass A: first guessed start (0xffffffff: none); pass B: verified start
+  uint32_t exit_[kWalkT];  // position after the segment's records
+  uint32_t cnt[kWalkT];    // records walked
+  uint32_t start2[kWalkT], exit2[kWalkT], cnt2[kWalkT];  // the second guess
+  uint32_t base[kWalkT];   // pass B: index of the segment's first record (0xffffffff: segment unused)
+  uint8_t fail[kWalkT], fail2[kWalkT];
+  uint32_t last_end;       // end of record count-1
+  int status;
+};
+
+// byteArrayPlainDecoder.next for records [0, count) of [p, p+n), the whole
+// block.  mode 0 (data page): out[i] = char end of value i = end(i) - 4 (i + 1);
+// mode 1 (dictionary page): out[i] = end(i), the next record's start.
+// Returns the status (all threads); *chars = sum of the lengths.
+__device__ int block_walk_g(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out, int mode, int64_t* chars,
+                            BlockWalkSharedG& sh) {
+  const int t = threadIdx.x;
+  const uint32_t L = ((n + kWalkT - 1) / kWalkT + 63) & ~63u;  // segment bytes (>= 64)
+  const uint32_t lo = (uint32_t)t * L < n ? (uint32_t)t * L : n;
+  const uint32_t hi = lo + L < n ? lo + L : n;
+  const uint32_t kNone = 0xffffffffu;
+  auto nop = [](uint32_t, uint32_t) {};
+  PQG_T(tp0);
+  // ---- pass A: guess two starts, walk the segment from each
+  // (a false start is typically the byte before a record — [c, len, 0, 0] reads
+  // as a short length — so the next candidate is usually the true record)
+  if (count > 0) {
+    uint32_t st = kNone, st2 = kNone;
+    if (t == 0) {
+      st = 0;
+    } else {
+      // positions whose length chain is valid for three records; a candidate
+      // is first screened on its own length (one 64-byte window load per 60
+      // positions), the deeper check walks from it
+      uintptr_t wb = 0;
+      uint4 g0 = make_uint4(0, 0, 0, 0), g1 = g0, g2 = g0, g3 = g0;
+      const uintptr_t pend = (uintptr_t)(p + n), lastg = (pend - 1) & ~(uintptr_t)15;
+      for (uint32_t q = lo; q < hi && n - q >= 4; q++) {
+        if (st != kNone && q > st + 64) break;
+        const uintptr_t a = (uintptr_t)(p + q);
+        if (a + 4 > wb + 64) {
+          wb = a & ~(uintptr_t)15;
+          g0 = ldg16(wb);
+          g1 = ldg16(wb + 16 < lastg ? wb + 16 : lastg);
+          g2 = ldg16(wb + 32 < lastg ? wb + 32 : lastg);
+          g3 = ldg16(wb + 48 < lastg ? wb + 48 : lastg);
+        }
+        const uint32_t off = (uint32_t)(a - wb), d = off >> 2, e1 = d + 1 < 16 ? d + 1 : 15;
+        const uint32_t w0 = pick4(pick4(g0.x, g0.y, g0.z, g0.w, d), pick4(g1.x, g1.y, g1.z, g1.w, d),
+                                  pick4(g2.x, g2.y, g2.z, g2.w, d), pick4(g3.x, g3.y, g3.z, g3.w, d), d >> 2);
+        const uint32_t w1 = pick4(pick4(g0.x, g0.y, g0.z, g0.w, e1), pick4(g1.x, g1.y, g1.z, g1.w, e1),
+                                  pick4(g2.x, g2.y, g2.z, g2.w, e1), pick4(g3.x, g3.y, g3.z, g3.w, e1), e1 >> 2);
+        const uint32_t l = __builtin_amdgcn_alignbit(w1, w0, (off & 3) * 8);
+        if ((int32_t)l < 0 || n - q - 4 < l) continue;
+        uint32_t e;
+        int f;
+        const uint32_t k = seg_walk(p, n, q, n, 3, &e, &f, nop);
+        if (k == 3 || (f && e == n)) {
+          if (st == kNone) {
+            st = q;
+          } else {
+            st2 = q;
+            break;
+          }
+        }
+      }
+    }
+    sh.start[t] = st;
+    sh.start2[t] = st2;
+    sh.fail[t] = sh.fail2[t] = 0;
+    sh.cnt[t] = sh.cnt2[t] = 0;
+    sh.exit_[t] = st;
+    sh.exit2[t] = st2;
+    uint32_t e;
+    int f;
+    if (st != kNone && st < hi) {
+      sh.cnt[t] = seg_walk(p, n, st, hi, 0xffffffffu, &e, &f, nop);
+      sh.exit_[t] = e;
+      sh.fail[t] = (uint8_t)f;
+    }
+    if (st2 != kNone && st2 < hi) {
+      sh.cnt2[t] = seg_walk(p, n, st2, hi, 0xffffffffu, &e, &f, nop);
+      sh.exit2[t] = e;
+      sh.fail2[t] = (uint8_t)f;
+    }
+  }
+  __syncthreads();
+  PQG_T(tp1);
+  // ---- thread 0: follow the true chain through the segments
+  if (t == 0) {
+    uint32_t redo = 0, redo_k = 0;
+    (void)redo;
+    (void)redo_k;
+    for (int s = 0; s < kWalkT; s++) sh.base[s] = kNone;
+    uint32_t cur = 0, idx = 0;
+    int status = kOK;
+    bool failed = false;
+    for (int s = 0; s < kWalkT && idx < count; s++) {
+      const uint32_t slo = (uint32_t)s * L < n ? (uint32_t)s * L : n;
+      const uint32_t shi = slo + L < n ? slo + L : n;
+      if (shi <= slo) break;     // past the end of the stream
+      if (cur >= shi) continue;  // a record spans the whole segment
+      uint32_t k, e;
+      int f;
+      if (sh.start[s] == cur) {  // a guess was right: take the segment's walk
+        k = sh.cnt[s];
+        e = sh.exit_[s];
+        f = sh.fail[s];
+      } else if (sh.start2[s] == cur) {
+        k = sh.cnt2[s];
+        e = sh.exit2[s];
+        f = sh.fail2[s];
+      } else {
+        k = seg_walk(p, n, cur, shi, 0xffffffffu, &e, &f, nop);
+        redo++;
+        redo_k += k;
+      }
+      sh.start[s] = cur;
+      sh.base[s] = idx;
+      idx += k;
+      cur = e;
+      if (f) {
+        failed = true;
+        break;
+      }
+    }
+    if (idx < count) {
+      // record `idx` at `cur` fails: fewer than 4 bytes (EOF), a negative
+      // length, or fewer bytes than its length (EOF)
+      status = kEOF;
+      if (failed && n - cur >= 4) {
+        const uint32_t l = (uint32_t)p[cur] | (uint32_t)p[cur + 1] << 8 | (uint32_t)p[cur + 2] << 16 |
+                           (uint32_t)p[cur + 3] << 24;
+        if ((int32_t)l < 0) status = kBYTE_ARRAY;
+      }
+    }
+    sh.status = status;
+    sh.last_end = 0;
+    PQG_ACC0(28, redo);
+    PQG_ACC0(29, redo_k);
+  }
+  __syncthreads();
+  PQG_T(tp2);
+  const int status = sh.status;
+  if (status != kOK) return status;
+  // ---- pass B: outputs from the verified starts
+  if (count > 0 && sh.base[t] != kNone && sh.base[t] < count) {
+    const uint32_t b = sh.base[t];
+    uint32_t e;
+    int f;
+    seg_walk(p, n, sh.start[t], hi, count - b, &e, &f,
+             [&](uint32_t k, uint32_t pos) {
+               const uint32_t i = b + k;
+               out[i] = mode ? (int64_t)pos : (int64_t)pos - 4 * ((int64_t)i + 1);
+               if (i == count - 1) sh.last_end = pos;
+             });
+  }
+  __syncthreads();
+  PQG_T(tp3);
+#ifdef PQG_PROFILE
+  PQG_ACC0(24, tp1 - tp0);
+  PQG_ACC0(25, tp2 - tp1);
+  PQG_ACC0(26, tp3 - tp2);
+  PQG_ACC0(27, 1);
+#endif
+  *chars = count ? (int64_t)sh.last_end - 4 * (int64_t)count : 0;
+  return kOK;
+}
+
 // ---- K7a ---------------------------------------------------------------------
 __global__ void __launch_bounds__(kWalkT) k_str_dict(JobDev* jobs, PageDev* pages, int64_t* doffs_arena) {
-  __shared__ BlockWalkShared sh;
+  __shared__ BlockWalkSharedG sh;
   JobDev& job = jobs[blockIdx.x];
   if (job.status == kCAPACITY || !(job.flags & 2) || job.dict_page < 0) return;
   PageDev& dp = pages[job.page_base + job.dict_page];
@@ -318,7 +540,7 @@ __global__ void __launch_bounds__(kWalkT) k_str_dict(JobDev* jobs, PageDev* page
   const int64_t cnt = dp.num_values;
   PQG_G int64_t* doffs = gmut(doffs_arena) + job.doffs_base;
   int64_t chars;
-  const int st = block_walk(gconst(job.dict_data), (uint32_t)job.dict_len, (uint32_t)cnt, doffs + 1, 1, &chars, sh);
+  const int st = block_walk_g(gconst(job.dict_data), (uint32_t)job.dict_len, (uint32_t)cnt, doffs + 1, 1, &chars, sh);
   if (threadIdx.x == 0) {
     if (st == kOK) {
       doffs[0] = 0;
@@ -922,12 +1144,29 @@ __device__ __forceinline__ void lds_copy(PQG_L uint8_t* dst, gcu8 src, int64_t l
   for (; k < len; k++) dst[k] = src[k];
 }
 
+// len bytes LDS -> LDS (any alignment): aligned dword reads, byte writes
+__device__ __forceinline__ void lds_copy_l(PQG_L uint8_t* dst, const PQG_L uint8_t* src, int64_t len) {
+  int64_t k = 0;
+  for (; k + 4 <= len; k += 4) {
+    const uint32_t a = (uint32_t)(uintptr_t)(src + k);
+    const PQG_L uint32_t* q = (const PQG_L uint32_t*)(src + k - (a & 3));
+    const uint32_t x = __builtin_amdgcn_alignbit(q[1], q[0], (a & 3) * 8);
+    dst[k] = (uint8_t)x;
+    dst[k + 1] = (uint8_t)(x >> 8);
+    dst[k + 2] = (uint8_t)(x >> 16);
+    dst[k + 3] = (uint8_t)(x >> 24);
+  }
+  for (; k < len; k++) dst[k] = src[k];
+}
+constexpr int kSrcStage = kCopyStage + 4 * 512 + 64;  // a PLAIN round's records: chars + length prefixes
+
 __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total,
                                                   int* queue, uint8_t* value_arena, int64_t* offs_arena) {
   __shared__ int s_t;
   __shared__ int64_t s_prev;  // page-relative end of the value before the round
   __shared__ int64_t part[9];
   __shared__ __attribute__((aligned(16))) uint8_t stage[kCopyStage];
+  __shared__ __attribute__((aligned(16))) uint8_t sstage[kSrcStage + 16];  // PLAIN / DLBA sources of a round
   const int n_items = total[kCtrItems];
   for (;;) {
     if (threadIdx.x == 0) s_t = queue_pull(queue);
@@ -984,7 +1223,35 @@ __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, 
       const uintptr_t abs_lo = (uintptr_t)(chars + r_lo), abs_hi = (uintptr_t)(chars + r_hi);
       const uintptr_t A0 = abs_lo & ~(uintptr_t)15;
       if (abs_hi - A0 <= (uintptr_t)kCopyStage) {
-        if (i < nn) {
+        // PLAIN / DLBA: the round's source bytes are contiguous in the page
+        // (records, or values back to back): staged in LDS with one round of
+        // coalesced loads, then every value is copied LDS -> LDS
+        const int64_t i_last = i0 + 512 < nn ? i0 + 511 : nn - 1;
+        const int64_t S_lo = dlba ? pg.cstart + r_lo : r_lo + 4 * (i0 + 1);
+        const int64_t S_hi = dlba ? pg.cstart + r_hi : r_hi + 4 * (i_last + 1);
+        const uintptr_t SA0 = (uintptr_t)(src + S_lo) & ~(uintptr_t)15;
+        const bool sstaged = !dict && S_hi > S_lo && (uintptr_t)(src + S_hi) - SA0 <= (uintptr_t)kSrcStage;
+        if (sstaged) {
+          const uintptr_t last = ((uintptr_t)(src + S_hi) - 1) & ~(uintptr_t)15;
+          constexpr int kSG = (kSrcStage + 16 + 16 * 512 - 1) / (16 * 512);
+          uint4 v[kSG];
+#pragma unroll
+          for (int k = 0; k < kSG; k++) {  // unconditional loads (clamped)
+            const uintptr_t g = SA0 + 16 * (uintptr_t)(threadIdx.x + 512 * k);
+            v[k] = ldg16(g < last ? g : last);
+          }
+#pragma unroll
+          for (int k = 0; k < kSG; k++) {
+            const uint32_t o = 16 * (threadIdx.x + 512 * k);
+            if (o < (uint32_t)(kSrcStage + 16)) sts16(lds_ptr(sstage) + o, v[k]);
+          }
+          __syncthreads();
+          if (i < nn) {
+            lds_copy_l(lds_ptr(stage) + ((uintptr_t)(chars + s0) - A0),
+                       lds_ptr(sstage) + ((uintptr_t)(src + from) - SA0), e - s0);
+            ends[i] = base + e;
+          }
+        } else if (i < nn) {
           lds_copy(lds_ptr(stage) + ((uintptr_t)(chars + s0) - A0), src + from, e - s0);
           ends[i] = base + e;
         }
@@ -992,7 +1259,7 @@ __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, 
         for (uintptr_t g = A0 + 16 * (uintptr_t)threadIdx.x; g < abs_hi; g += 16 * 512) {
           const u32x4_t v = *(const PQG_L u32x4_t*)(lds_ptr(stage) + (g - A0));
           if (g >= abs_lo && g + 16 <= abs_hi) {
-            stg16(g, make_uint4(v.x, v.y, v.z, v.w));
+            stg16o(g, make_uint4(v.x, v.y, v.z, v.w));
           } else {
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
             for (int b = 0; b < 16; b++)

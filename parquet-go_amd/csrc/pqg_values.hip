@@ -122,8 +122,8 @@ struct DictSink {
         const uintptr_t o = (uintptr_t)(out + (int64_t)i0[b] * 4);
         if (cnt[b] == 8 && (o & 15) == 0 && ok[b][0] && ok[b][1] && ok[b][2] && ok[b][3] && ok[b][4] && ok[b][5] &&
             ok[b][6] && ok[b][7]) {
-          stg16(o, make_uint4(gv[b][0], gv[b][1], gv[b][2], gv[b][3]));
-          stg16(o + 16, make_uint4(gv[b][4], gv[b][5], gv[b][6], gv[b][7]));
+          stg16o(o, make_uint4(gv[b][0], gv[b][1], gv[b][2], gv[b][3]));
+          stg16o(o + 16, make_uint4(gv[b][4], gv[b][5], gv[b][6], gv[b][7]));
         } else {
 #pragma unroll
           for (int q = 0; q < 8; q++)
@@ -363,8 +363,8 @@ __device__ __forceinline__ void store_run64(uintptr_t base, const uint64_t (&v)[
   const uintptr_t o = base + 32 * (uintptr_t)lane;
   if (!shifted) {
     if (Full || nv == 4) {
-      stg16(o, make_uint4((uint32_t)v[0], (uint32_t)(v[0] >> 32), (uint32_t)v[1], (uint32_t)(v[1] >> 32)));
-      stg16(o + 16, make_uint4((uint32_t)v[2], (uint32_t)(v[2] >> 32), (uint32_t)v[3], (uint32_t)(v[3] >> 32)));
+      stg16o(o, make_uint4((uint32_t)v[0], (uint32_t)(v[0] >> 32), (uint32_t)v[1], (uint32_t)(v[1] >> 32)));
+      stg16o(o + 16, make_uint4((uint32_t)v[2], (uint32_t)(v[2] >> 32), (uint32_t)v[3], (uint32_t)(v[3] >> 32)));
     } else {
 #pragma unroll
       for (int k = 0; k < 4; k++)
@@ -376,8 +376,8 @@ __device__ __forceinline__ void store_run64(uintptr_t base, const uint64_t (&v)[
   const uint32_t n1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v[0] >> 32), 0x130, 0xf, 0xf, true);
   const int nxv = Full ? 4 : __builtin_amdgcn_update_dpp(0, nv, 0x130, 0xf, 0xf, true);
   if (Full ? lane < 63 : (nv == 4 && nxv >= 1)) {
-    stg16(o + 8, make_uint4((uint32_t)v[1], (uint32_t)(v[1] >> 32), (uint32_t)v[2], (uint32_t)(v[2] >> 32)));
-    stg16(o + 24, make_uint4((uint32_t)v[3], (uint32_t)(v[3] >> 32), n0, n1));
+    stg16o(o + 8, make_uint4((uint32_t)v[1], (uint32_t)(v[1] >> 32), (uint32_t)v[2], (uint32_t)(v[2] >> 32)));
+    stg16o(o + 24, make_uint4((uint32_t)v[3], (uint32_t)(v[3] >> 32), n0, n1));
   } else {
 #pragma unroll
     for (int k = 1; k < 4; k++)
