@@ -73,7 +73,7 @@ constexpr int kWinLit = 1024;     // literals up to this many bytes (after the g
 #define PQG_SNAPPY_WPE 3  // waves per EU the decoder is compiled for (3: <= 168 VGPRs, no spills)
 #endif
 #ifndef PQG_SNAPPY_LL_UNCOND
-#define PQG_SNAPPY_LL_UNCOND 1  // long literals: unconditional piece loads (36 B of spills at 168 VGPRs)
+#define PQG_SNAPPY_LL_UNCOND 0  // 1: unconditional long-literal piece loads (36 B of spills at 168 VGPRs; C4 snappy 9.9 -> 10.7 ms)
 #endif
 #ifndef PQG_SNAPPY_SERIAL_CHAIN
 #define PQG_SNAPPY_SERIAL_CHAIN 0
@@ -343,7 +343,7 @@ struct SnapBlock {
 
   // A literal too long for one batch (or whose bytes leave the window):
   // pieces of up to kLongPiece bytes straight from the compressed block.
-  __device__ __attribute__((noinline)) void long_literal(int64_t at, int64_t len) {
+  __device__ void long_literal(int64_t at, int64_t len) {
     const int lane = lane_id();
     constexpr int NG = kLongPiece / 1024;  // granules per lane
     while (len > 0) {

@@ -1144,6 +1144,29 @@ __device__ __forceinline__ void lds_copy(PQG_L uint8_t* dst, gcu8 src, int64_t l
   for (; k < len; k++) dst[k] = src[k];
 }
 
+// A value of <= 32 bytes from global src to LDS dst: its (at most 10)
+// aligned source dwords are loaded together, unconditionally (clamped to the
+// value's last dword), so a round of values costs one round trip instead of
+// one per 4 bytes (the dictionary gathers of k_str_copy)
+__device__ __forceinline__ void lds_copy_short(PQG_L uint8_t* dst, gcu8 src, int64_t len) {
+  const uintptr_t a = (uintptr_t)src, base = a & ~(uintptr_t)3;
+  const uintptr_t last = len > 0 ? (a + (uintptr_t)len - 1) & ~(uintptr_t)3 : base;
+  const uint32_t sh = (uint32_t)(a & 3) * 8;
+  uint32_t w[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    const uintptr_t q = base + 4 * (uintptr_t)k;
+    w[k] = *(const PQG_G uint32_t*)(q < last ? q : last);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t x = sh ? __builtin_amdgcn_alignbit(w[k + 1], w[k], sh) : w[k];
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+      if (4 * k + b < len) dst[4 * k + b] = (uint8_t)(x >> (8 * b));
+  }
+}
+
 // len bytes LDS -> LDS (any alignment): aligned dword reads, byte writes
 __device__ __forceinline__ void lds_copy_l(PQG_L uint8_t* dst, const PQG_L uint8_t* src, int64_t len) {
   int64_t k = 0;
@@ -1252,7 +1275,9 @@ __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, 
             ends[i] = base + e;
           }
         } else if (i < nn) {
-          lds_copy(lds_ptr(stage) + ((uintptr_t)(chars + s0) - A0), src + from, e - s0);
+          PQG_L uint8_t* d = lds_ptr(stage) + ((uintptr_t)(chars + s0) - A0);
+          if (e - s0 <= 32) lds_copy_short(d, src + from, e - s0);
+          else lds_copy(d, src + from, e - s0);
           ends[i] = base + e;
         }
         __syncthreads();

@@ -7,9 +7,13 @@ FETCH_SIZE is calibrated on this run's own known-byte kernel: k_page_cands
 reads every chunk byte exactly once with 16-byte-per-lane loads, so
 factor = bytes_in / FETCH_SIZE(k_page_cands) (MI355X_MICROARCH.md: gfx950
 reports 1/2 of such streaming reads, factor ~2).  `fetch` applies that factor
-to every kernel (narrower or gathered loads are uncalibrated; `fetch_raw` keeps
-the counter as read).  WRITE_SIZE is exact for 16-byte streaming stores and
-taken as is."""
+to every kernel; `fetch_raw` keeps the counter as read.  tools/fetch_calib.hip
+(profiles/r04/fetch_calib) checks the other widths the kernels use: 4-byte
+coalesced loads report the same 1/2; 4-byte random gathers from a 256 KiB or
+a 4 MiB table report only the table's compulsory misses (8 XCDs x table / 2):
+gathers served by L2 never reach the counter, so a gather kernel's fetch above
+its streams is lines re-fetched from the Infinity Cache after eviction.
+WRITE_SIZE is exact for 16-byte streaming stores and taken as is."""
 import collections
 import csv
 import json
