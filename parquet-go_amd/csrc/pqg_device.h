@@ -31,6 +31,11 @@ __device__ __forceinline__ uint4 ldg16(uintptr_t a) {
   const u32x4_t v = *(const PQG_G u32x4_t*)a;
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// streaming read (non-temporal): data read once, kept out of the L2's way
+__device__ __forceinline__ uint4 ldg16_nt(uintptr_t a) {
+  const u32x4_t v = __builtin_nontemporal_load((const PQG_G u32x4_t*)a);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ void stg16(uintptr_t a, uint4 x) {
   const u32x4_t v = {x.x, x.y, x.z, x.w};
   *(PQG_G u32x4_t*)a = v;

@@ -116,6 +116,9 @@ struct DProf {
 #ifndef PQG_DICT_NT
 #define PQG_DICT_NT PQG_NT_OUT
 #endif
+#ifndef PQG_DICT_NT_IN
+#define PQG_DICT_NT_IN 0  // 1: the index-stream stage loads non-temporal too (an experiment switch)
+#endif
 __device__ __forceinline__ void dict_store(PQG_G uint32_t* p, uint32_t v) {
 #if PQG_DICT_NT
   __builtin_nontemporal_store(v, p);
@@ -266,7 +269,11 @@ __device__ __forceinline__ int64_t dict_page(PieceShared& ps, const gcu8 sp, con
 #pragma unroll
     for (int k = 0; k < kPG; k++) {  // unconditional loads (see dbp_restage): zeroed when stored
       const int64_t at = plo + 16 * (int64_t)(lane + 64 * k);
+#if PQG_DICT_NT_IN
+      pg[k] = ldg16_nt(at < n ? (uintptr_t)(sp + at) : (pa & ~(uintptr_t)15));  // index bytes: read once
+#else
       pg[k] = ldg16(at < n ? (uintptr_t)(sp + at) : (pa & ~(uintptr_t)15));
+#endif
     }
 #pragma unroll
     for (int k = 0; k < kPRunGr; k++) sts16(lds_ptr(ps.runs) + 2 * (lane + 64 * k), rg[k]);

@@ -621,34 +621,44 @@ __global__ void __launch_bounds__(1024) k_page_chain(JobDev* jobs, PageDev* page
   const int n = s_n, mode = s_mode, cut = s_cut, nok = s_nok, extra = s_extra;
   const int nw = n < job.page_cap ? n : job.page_cap;
   int64_t slot_carry = 0, scratch_carry = 0;
+  // Rounds of 1024 pages, software-pipelined: the next round's candidate
+  // records are loaded before this round's page records are stored (a load
+  // issued after the stores would wait for them: vmcnt counts both in order).
+  // Loads are unconditional (the page index clamped to n - 1).
+  auto fetch = [&](int k, Cand& c) {
+    const int kk = k < n ? k : n - 1;
+    const int sl = mode == 1 ? order[job.page_base + kk] : (kk < nok ? o2s[kk] : extra);
+    c = cands[cb + sl];
+  };
+  Cand cur;
+  if (n > 0) fetch(tid, cur);
   for (int b0 = 0; b0 < n; b0 += 1024) {
     const int k = b0 + tid;
     int64_t nv = 0, cp = 0;
     int st = kOK;
-    const Cand* cd = nullptr;
     if (k < n) {
-      const int sl = mode == 1 ? order[job.page_base + k] : (k < nok ? o2s[k] : extra);
-      cd = &cands[cb + sl];
-      st = (k == cut) ? kDICT_PAGE : cd->status;
-      cp = (k == cut) ? 0 : cd->comp;
-      if ((cd->type == 0 || cd->type == 3) && st == kOK) nv = cd->num_values;
+      st = (k == cut) ? kDICT_PAGE : cur.status;
+      cp = (k == cut) ? 0 : cur.comp;
+      if ((cur.type == 0 || cur.type == 3) && st == kOK) nv = cur.num_values;
       if (st != kOK) s_status = st;  // only the last page can fail
     }
     int64_t tot_nv, tot_cp;
     const int64_t ex_nv = block_excl_scan<1024>(nv, &tot_nv, part);
     const int64_t ex_cp = block_excl_scan<1024>(cp, &tot_cp, part);
+    Cand nxt;
+    if (b0 + 1024 < n) fetch(b0 + 1024 + tid, nxt);
     if (k < nw) {
       PageDev pg;
-      init_page(pg, j, cd->pos, cd->payload);
-      pg.page_type = cd->type;
-      pg.encoding = cd->encoding;
-      pg.num_values = cd->num_values;
-      pg.csize = cd->csize;
-      pg.usize = cd->usize;
-      pg.def_len = cd->def_len;
-      pg.rep_len = cd->rep_len;
-      pg.def_enc = cd->def_enc;
-      pg.rep_enc = cd->rep_enc;
+      init_page(pg, j, cur.pos, cur.payload);
+      pg.page_type = cur.type;
+      pg.encoding = cur.encoding;
+      pg.num_values = cur.num_values;
+      pg.csize = cur.csize;
+      pg.usize = cur.usize;
+      pg.def_len = cur.def_len;
+      pg.rep_len = cur.rep_len;
+      pg.def_enc = cur.def_enc;
+      pg.rep_enc = cur.rep_enc;
       pg.read_status = st;
       pg.slot_offset = slot_carry + ex_nv;
       if (cp > 0) pg.scratch_offset = scratch_carry + ex_cp;
@@ -656,6 +666,7 @@ __global__ void __launch_bounds__(1024) k_page_chain(JobDev* jobs, PageDev* page
     }
     slot_carry += tot_nv;
     scratch_carry += tot_cp;
+    cur = nxt;
   }
   __syncthreads();
   if (tid == 0) {
@@ -774,27 +785,40 @@ __global__ void __launch_bounds__(1024) k_page_list(JobDev* jobs, PageDev* pages
   JobDev& job = jobs[j];
   const int n = pages_of(j);
   int64_t rc = 0, bc = 0;
+  // rounds of 1024 pages, the next round's page fields loaded (unconditionally,
+  // index clamped) before this round's stores: see k_page_chain
+  struct F { int32_t type, usize, csize, nv; int64_t so; };
+  auto fetch = [&](int i, F& f) {
+    const PageDev& pg = pages[job.page_base + (i < n ? i : n - 1)];
+    f.type = pg.page_type;
+    f.usize = pg.usize;
+    f.csize = pg.csize;
+    f.nv = pg.num_values;
+    f.so = pg.scratch_offset;
+  };
+  F cur;
+  if (n > 0) fetch((int)threadIdx.x, cur);
   for (int b = 0; b < n; b += 1024) {
     const int i = b + threadIdx.x;
     int64_t nr = 0, nb = 0;
-    if (i < n) {
-      if (off + i < list_cap) list[off + i] = (int)(job.page_base + i);
-      PageDev& pg = pages[job.page_base + i];
-      if (pg.page_type == 0 || pg.page_type == 3) {
-        const int64_t B = pg.scratch_offset >= 0 ? (int64_t)(uint32_t)pg.usize : (int64_t)(uint32_t)pg.csize;
-        nr = B / 2 + 2;
-        nb = (int64_t)(uint32_t)pg.num_values / kHBlock + nr / kHBlockRuns + B / (kHBlockBytes / 2) + 3;
-      }
+    if (i < n && (cur.type == 0 || cur.type == 3)) {
+      const int64_t B = cur.so >= 0 ? (int64_t)(uint32_t)cur.usize : (int64_t)(uint32_t)cur.csize;
+      nr = B / 2 + 2;
+      nb = (int64_t)(uint32_t)cur.nv / kHBlock + nr / kHBlockRuns + B / (kHBlockBytes / 2) + 3;
     }
     int64_t tr, tb;
     const int64_t er = block_excl_scan<1024>(nr, &tr, part);
     const int64_t eb = block_excl_scan<1024>(nb, &tb, part);
+    F nxt;
+    if (b + 1024 < n) fetch(b + 1024 + (int)threadIdx.x, nxt);
     if (i < n) {
+      if (off + i < list_cap) list[off + i] = (int)(job.page_base + i);
       pages[job.page_base + i].run_off = rc + er;
       pages[job.page_base + i].blk_off = bc + eb;
     }
     rc += tr;
     bc += tb;
+    cur = nxt;
   }
   if (threadIdx.x == 0) {
     job.run_used = rc;

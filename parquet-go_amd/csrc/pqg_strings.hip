@@ -590,14 +590,31 @@ struct StrDictCount {
   int64_t bad;   // first value index with an invalid key
   int64_t sum;   // lane's chars
   __device__ __forceinline__ void prepare(const uint32_t (&)[kGroup][8], const uint32_t (&)[kGroup], const int (&)[kGroup]) {}
+  // every entry-offset gather of the group is issued first, unconditionally
+  // (a key past the dictionary or a value past cnt reads entry 0), then the
+  // keys are parked and the lengths summed: one round trip per group instead
+  // of one per value (a guarded load is waited for inside its branch, and a
+  // load issued after the key stores would wait for them)
   __device__ __forceinline__ void group(const uint32_t (&v)[kGroup][8], const uint32_t (&i0)[kGroup],
                                         const int (&cnt)[kGroup]) {
+    int64_t a[kGroup][8], c[kGroup][8];
 #pragma unroll
     for (int b = 0; b < kGroup; b++)
-      for (int q = 0; q < cnt[b]; q++) {
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const uint32_t key = v[b][q];
+        const uint32_t kc = (q < cnt[b] && (int64_t)key < count) ? key : 0u;
+        a[b][q] = doffs[kc];
+        c[b][q] = doffs[kc + 1];
+      }
+#pragma unroll
+    for (int b = 0; b < kGroup; b++)
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        if (q >= cnt[b]) continue;
         const uint32_t key = v[b][q];
         keys[i0[b] + q] = key;
-        if ((int64_t)key < count) sum += doffs[key + 1] - doffs[key] - 4;
+        if ((int64_t)key < count) sum += c[b][q] - a[b][q] - 4;
         else if ((int64_t)(i0[b] + q) < bad) bad = (int64_t)(i0[b] + q);
       }
   }
@@ -1222,11 +1239,14 @@ __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, 
       const int64_t r_lo = s_prev;  // the round's first byte (read before any barrier moves it)
       int64_t e = 0, s0 = 0, from = 0;
       if (dict) {
+        // unconditional loads (the value index clamped to nn - 1): a load
+        // under a branch is waited for inside it
+        const int64_t key = ends[i < nn ? i : nn - 1];
+        const int64_t f0 = doffs[key] + 4, f1 = doffs[key + 1];
         int64_t len = 0;
         if (i < nn) {
-          const int64_t key = ends[i];
-          from = doffs[key] + 4;
-          len = doffs[key + 1] - from;
+          from = f0;
+          len = f1 - f0;
         }
         int64_t tot;
         s0 = r_lo + block_excl_scan<512>(len, &tot, part);
