@@ -23,7 +23,7 @@ def main(out_dir, tag, configs):
             print(cfg, "missing PMC outputs")
             continue
         d = json.loads(open(line).read().strip().splitlines()[-1])
-        workload = d["config"]["workload"]
+        workload = d["workload"] if "workload" in d else d["config"]["workload"]
         bytes_in = d["roofline"]["stage_alg_bytes"]["scan"]
         pmc_traffic.main(fetch, write, os.path.join(root, "profiles", "%s_pmc_%s.json" % (tag, cfg)), workload,
                          bytes_in)
