@@ -429,28 +429,26 @@ struct SnapBlock {
     const int64_t a0 = d & ~(int64_t)15;
     const int pre = (int)(d - a0);
     const int lim = pre + (int)len;
-    if (16 * lane < lim) {
-      // source bytes of the granule: window offsets [wo - pre + 16 lane, +16)
-      // (lane 0 may start up to 15 bytes before the window: those bytes are
-      // the granule's history prefix, replaced below; the reads stay in LDS)
-      const int so = (int)wo - pre + 16 * lane;
-      const PQG_L uint32_t* q = (const PQG_L uint32_t*)(lds_ptr(sh->in) + (so & ~3));
-      const uint32_t sft = (uint32_t)(so & 3) * 8;
-      const uint32_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3], x4 = q[4];
-      uint32_t w[4] = {__builtin_amdgcn_alignbit(x1, x0, sft), __builtin_amdgcn_alignbit(x2, x1, sft),
-                       __builtin_amdgcn_alignbit(x3, x2, sft), __builtin_amdgcn_alignbit(x4, x3, sft)};
-      const uint32_t rp = (uint32_t)((a0 + 16 * lane) & (kRing - 1));
-      if (lane == 0 && pre > 0) {  // keep the history bytes before d
-        const u32x4_t old = *(const PQG_L u32x4_t*)(lds_ptr(sh->ring) + rp);
-        const uint32_t ow[4] = {old.x, old.y, old.z, old.w};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int keep = pre - 4 * k;  // bytes of this dword before d
-          const uint32_t m = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : (0xffffffffu >> (8 * (4 - keep)));
-          w[k] = (ow[k] & m) | (w[k] & ~m);
-        }
-      }
-      sts16(lds_ptr(sh->ring) + rp, make_uint4(w[0], w[1], w[2], w[3]));
+    // A ragged first granule (pre > 0) is written byte by byte by lanes
+    // pre..15, one byte each, so that its history bytes before d are never
+    // read back (a read-modify-write would put a second LDS round trip on
+    // every literal of the tag-by-tag path); the other granules go whole.
+    // Both sets of source reads are issued before either write.
+    const int so = (int)wo - pre + 16 * lane;
+    const bool whole = 16 * lane < lim && (lane > 0 || pre == 0);
+    const bool head = pre > 0 && lane >= pre && lane < 16 && lane < lim;
+    // (lane 0 of a ragged literal may start up to 15 bytes before the window:
+    // those offsets are clamped, the bytes are not written)
+    const int hso = (int)wo - pre + lane;
+    const PQG_L uint32_t* q = (const PQG_L uint32_t*)(lds_ptr(sh->in) + ((whole ? so : 0) & ~3));
+    const uint32_t sft = (uint32_t)(so & 3) * 8;
+    const uint32_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3], x4 = q[4];
+    const uint8_t hb = lds_ptr(sh->in)[head ? hso : 0];
+    if (head) lds_ptr(sh->ring)[(uint32_t)(a0 + lane) & (kRing - 1)] = hb;
+    if (whole) {
+      const uint32_t w[4] = {__builtin_amdgcn_alignbit(x1, x0, sft), __builtin_amdgcn_alignbit(x2, x1, sft),
+                             __builtin_amdgcn_alignbit(x3, x2, sft), __builtin_amdgcn_alignbit(x4, x3, sft)};
+      sts16(lds_ptr(sh->ring) + ((a0 + 16 * lane) & (kRing - 1)), make_uint4(w[0], w[1], w[2], w[3]));
     }
     d += len;
   }
@@ -481,6 +479,20 @@ struct SnapBlock {
     d += len;
   }
 
+  // peek8 in two halves: the LDS loads, then (after other work has been
+  // issued behind them) the funnel shift and the move to scalar registers
+  struct Peek {
+    uint32_t a, b, c, sft;
+  };
+  __device__ __forceinline__ Peek peek_issue(int64_t t) {
+    const uint32_t o = (uint32_t)(t - in_base);
+    const PQG_L uint32_t* q = (const PQG_L uint32_t*)(lds_ptr(sh->in) + (o & ~3u));
+    return Peek{q[0], q[1], q[2], (o & 3) * 8};
+  }
+  __device__ __forceinline__ uint64_t peek_finish(const Peek& p) {
+    const uint32_t lo = __builtin_amdgcn_alignbit(p.b, p.a, p.sft), hi = __builtin_amdgcn_alignbit(p.c, p.b, p.sft);
+    return (uint64_t)__builtin_amdgcn_readfirstlane(lo) | (uint64_t)__builtin_amdgcn_readfirstlane(hi) << 32;
+  }
   // 8 bytes at block offset t (inside the window): one broadcast LDS load
   __device__ __forceinline__ uint64_t peek8(int64_t t) {
     const uint32_t o = (uint32_t)(t - in_base);
@@ -535,7 +547,9 @@ struct SnapBlock {
       }
       short_streak = length < 16 ? short_streak + 1 : 0;
       const bool next_in = ns < slen && ns >= in_base && ns + kSnWinNeed <= in_base + kSnWin;
-      const uint64_t nx8 = next_in ? peek8(ns) : 0;
+      // the next header's loads go out ahead of this tag's bytes and are
+      // waited for after them (one LDS round trip per tag, not two)
+      const Peek nx = peek_issue(next_in ? ns : in_base);
       if (lit) {
         const int64_t at = s + hdr;
         if ((d & 15) + length <= kWinLit && at + length <= in_base + kSnWin) window_literal((uint32_t)(at - in_base), length);
@@ -546,7 +560,7 @@ struct SnapBlock {
       maybe_flush();  // keeps the unflushed tail inside the ring
       s = ns;
       if (!next_in) break;
-      x8 = nx8;
+      x8 = peek_finish(nx);
     }
     if ((d & ~(int64_t)15) - flushed >= kSnFlush) flush(d & ~(int64_t)15);
     return kOK;

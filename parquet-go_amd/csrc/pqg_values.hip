@@ -570,7 +570,18 @@ __device__ __forceinline__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, b
   const uint64_t wmask_mbc = mbc >= 8 ? ~0ull : (1ull << (8 * mbc)) - 1;
   const uint64_t wadd = 0x0101010101010101ull * (uint64_t)(127 - maxw);
   const int32_t mb_bytes_per_w = mbvc / 8;  // bytes of a miniblock per bit of width
+  int64_t spec_len = 0;  // length of the last block walked one at a time (0: none, or a partial one)
+#ifdef PQG_PROFILE
+  uint64_t pf_rs = 0, pf_walk = 0, pf_tile = 0, pf_nrs = 0, pf_nb = 0;
+#define PQG_DBP_RS(...) { PQG_T(ra_); __VA_ARGS__; PQG_T(rb_); pf_rs += rb_ - ra_; pf_nrs++; }
+#else
+#define PQG_DBP_RS(...) { __VA_ARGS__; }
+#endif
   while (p0 < P) {
+#ifdef PQG_PROFILE
+    PQG_T(tw0_);
+    const uint64_t rs0_ = pf_rs;
+#endif
     int nb = 0;
     int64_t p_end = p0;
     bool fresh = false;  // the stage was just filled at blk_pos
@@ -578,8 +589,64 @@ __device__ __forceinline__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, b
       // the header (<= 10 varint bytes + mbc widths) must be staged
       if (!(blk_pos >= st_lo && blk_pos + 10 + mbc <= st_hi)) {
         if (nb > 0) break;  // decode the batch so far, then restage here
-        dbp_restage(s, n, stb, blk_pos, st_lo, st_hi);
+        PQG_DBP_RS(dbp_restage(s, n, stb, blk_pos, st_lo, st_hi));
         fresh = true;
+      }
+      // Speculative headers: lane i reads a header at blk_pos + i * spec_len
+      // (spec_len: the length of the last block walked one at a time; the
+      // blocks of a page are usually all the same length).  The blocks before
+      // the first lane whose guess fails — a length other than spec_len, a
+      // header or body not staged, a header the exact walk below would reject,
+      // the batch's or the positions' end — are taken at once; a failed first
+      // lane leaves that block to the exact walk.
+      if (spec_len > 0) {
+        const int64_t q = blk_pos + (int64_t)lane * spec_len;
+        bool ok = q + spec_len <= st_hi && q + 10 + mbc <= st_hi && q + spec_len <= n && nb + lane < kBlocks &&
+                  p_end + (int64_t)(lane + 1) * bs <= P;
+        const uint32_t hr = (uint32_t)((ok ? q : blk_pos) - st_lo);
+        uint32_t h[7];
+#pragma unroll
+        for (int k = 0; k < 7; k++) h[k] = stw[(hr >> 2) + k];
+        const uint32_t hs = (hr & 3) * 8;
+        uint64_t x0 = (uint64_t)h[0] | (uint64_t)h[1] << 32, x1 = (uint64_t)h[2] | (uint64_t)h[3] << 32;
+        const uint64_t x2 = (uint64_t)h[4] | (uint64_t)h[5] << 32;
+        if (hs) {
+          x0 = (x0 >> hs) | (x1 << (64 - hs));
+          x1 = (x1 >> hs) | (x2 << (64 - hs));
+        }
+        const uint64_t cont = ~x0 & 0x8080808080808080ull;
+        ok = ok && cont != 0;  // a varint of <= 8 bytes
+        const int vl = cont ? (int)(__builtin_ctzll(cont) >> 3) + 1 : 1;
+        uint64_t t = x0 & 0x7f7f7f7f7f7f7f7full;
+        t = (t & 0x007f007f007f007full) | ((t & 0x7f007f007f007f00ull) >> 1);
+        t = (t & 0x00003fff00003fffull) | ((t & 0x3fff00003fff0000ull) >> 2);
+        t = (t & 0x000000000fffffffull) | ((t & 0x0fffffff00000000ull) >> 4);
+        const uint64_t ux = vl == 8 ? t : t & ((1ull << (7 * vl)) - 1);
+        int64_t mdv = (int64_t)(ux >> 1);
+        if (ux & 1) mdv = ~mdv;
+        if (!is64 && (mdv > 2147483647LL || mdv < -2147483648LL)) ok = false;
+        const uint32_t vs = (uint32_t)vl * 8;  // 8..64
+        uint64_t wpk = vs < 64 ? (x0 >> vs) | (x1 << (64 - vs)) : x1;
+        wpk &= wmask_mbc;
+        if (((wpk | ((wpk & 0x7f7f7f7f7f7f7f7full) + wadd)) & 0x8080808080808080ull) != 0) ok = false;
+        uint64_t sw = (wpk & 0x00ff00ff00ff00ffull) + ((wpk >> 8) & 0x00ff00ff00ff00ffull);
+        sw += sw >> 16;
+        sw += sw >> 32;
+        const int64_t body = q + vl + mbc;
+        ok = ok && body + (int64_t)mb_bytes_per_w * (int64_t)((uint32_t)sw & 0xffff) == q + spec_len;
+        const uint64_t fail = __ballot(!ok);
+        const int k = fail ? __ffsll((long long)fail) - 1 : 64;
+        if (k > 0) {
+          if (lane < k) {
+            sh.mind[nb + lane] = (uint64_t)mdv;
+            sh.wpk[nb + lane] = wpk;
+            sh.sbody[nb + lane] = (uint32_t)(body - st_lo);
+          }
+          nb += k;
+          p_end += (int64_t)k * bs;
+          blk_pos += (int64_t)k * spec_len;
+          continue;
+        }
       }
       // block header (readMiniBlockHeader): its <= 10 varint bytes and <= 8
       // widths come from one read of 7 stage dwords, made wave-uniform
@@ -663,7 +730,7 @@ __device__ __forceinline__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, b
         if (nb > 0) break;
         if (fresh) return dbp_decode_rest(s, n, readable, is64, nn, out, sh, P, p0, blk_pos, carry, bs, mbc, mbvc,
                                           total, pow2, bs_sh, mb_sh);
-        dbp_restage(s, n, stb, blk_pos, st_lo, st_hi);
+        PQG_DBP_RS(dbp_restage(s, n, stb, blk_pos, st_lo, st_hi));
         fresh = true;
         continue;
       }
@@ -673,10 +740,16 @@ __device__ __forceinline__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, b
         sh.sbody[nb] = (uint32_t)(body - st_lo);  // stage byte of the first miniblock
       }
       nb++;
+      spec_len = bp1 - bp0 == bs ? off - blk_pos : 0;
       p_end = bp1;
       blk_pos = off;
     }
     __builtin_amdgcn_wave_barrier();
+#ifdef PQG_PROFILE
+    PQG_T(tw1_);
+    pf_walk += (tw1_ - tw0_) - (pf_rs - rs0_);
+    pf_nb += nb;
+#endif
     // unpack + wrapping prefix over positions [p0, p_end): value(p) = carry + sum of deltas.
     // A lane's 4 positions share one miniblock (mbvc % 8 == 0): the block /
     // miniblock split once per lane, by shifts for power-of-two sizes.
@@ -685,8 +758,20 @@ __device__ __forceinline__ int dbp_decode(gcu8 s, int64_t n, int64_t readable, b
       carry = dbp_tile<true>(sh, stw, t0, p0, p_end, pow2, bs_sh, mb_sh, bs, mbvc, carry, is64, out);
     if (t0 < p_end) carry = dbp_tile<false>(sh, stw, t0, p0, p_end, pow2, bs_sh, mb_sh, bs, mbvc, carry, is64, out);
     __builtin_amdgcn_wave_barrier();
+#ifdef PQG_PROFILE
+    PQG_T(tw2_);
+    pf_tile += tw2_ - tw1_;
+#endif
     p0 = p_end;
   }
+#ifdef PQG_PROFILE
+  PQG_ACC(20, 0, pf_walk);
+  PQG_ACC(21, 0, pf_rs);
+  PQG_ACC(22, 0, pf_tile);
+  PQG_ACC(23, 0, pf_nrs);
+  PQG_ACC(24, 0, pf_nb);
+#endif
+#undef PQG_DBP_RS
   if (nn > total) return kEOF;
   return kOK;
 }
