@@ -283,21 +283,30 @@ __device__ void chain_walk(gcu8 src, int64_t slen, int64_t hi, int64_t& x, uint3
   chain_walk_rd(GlobalRd8{src, slen}, slen, hi, x, acc);
 }
 
+// SnapBlock keeps 32-bit block offsets: blocks (compressed or not) longer
+// than this are UNSUPPORTED (page sizes are int32 in the page header; this
+// leaves 1 MiB of headroom for the window and batch arithmetic)
+constexpr int64_t kSnMaxLen = 0x7ff00000;
+constexpr int32_t kSnNoWindow = -(1 << 30);  // in_base before the first fill
+
 struct SnapBlock {
   gcu8 src;
-  int64_t slen;
+  int32_t slen;
   gu8 dst;
-  int64_t dlen;
+  int32_t dlen;
   SnapShared* sh;
-  int64_t d = 0;        // output bytes produced
-  int64_t flushed = 0;  // output bytes stored (16-aligned until the end)
-  int64_t in_base = kFarAway;
+  // Block offsets and lengths are 32-bit (both lengths <= kSnMaxLen, checked
+  // by the kernels): the scalar bookkeeping of every tag is then one
+  // instruction per operation instead of a 64-bit pair or a VALU compare.
+  int32_t d = 0;        // output bytes produced
+  int32_t flushed = 0;  // output bytes stored (16-aligned until the end)
+  int32_t in_base = kSnNoWindow;
   // A sub-block decode (k_snap_decode) produces the output [base, dend) only
   // and may read no output before base; the whole block is base 0, dend dlen.
   // Any tag that cannot be decoded that way (corrupt, or a copy reaching
   // before base) fails the decode, and the page is decoded serially.
-  int64_t base = 0;
-  int64_t dend = -1;
+  int32_t base = 0;
+  int32_t dend = -1;
 #ifdef PQG_PROFILE
   uint64_t pacc[16] = {0};
 #define PQG_ST(v) const uint64_t v = __builtin_amdgcn_s_memtime()
@@ -308,13 +317,13 @@ struct SnapBlock {
 #endif
 
   // window [in_base, in_base + kSnWin) over the compressed block, 16-aligned in memory
-  __device__ void fill(int64_t at) {
+  __device__ void fill(int32_t at) {
     const int lane = lane_id();
-    in_base = at - (int64_t)(((uintptr_t)(src + at)) & 15);
+    in_base = at - (int32_t)(((uintptr_t)(src + at)) & 15);
     uint4 v[kSnWin / 1024];
 #pragma unroll
     for (int h = 0; h < kSnWin / 1024; h++) {
-      const int64_t g = in_base + 1024 * h + 16 * lane;
+      const int32_t g = in_base + 1024 * h + 16 * lane;
       // a granule holding a byte of [0, slen) is mapped (these loads stay
       // guarded: unconditional ones push the decoder past its 168 VGPRs; the
       // refills are ~1 % of its time, r04 session 10 counters)
@@ -327,42 +336,42 @@ struct SnapBlock {
   }
 
   // store ring granules [flushed, upto) to dst (upto 16-aligned, or the end)
-  __device__ void flush(int64_t upto) {
+  __device__ void flush(int32_t upto) {
     const int lane = lane_id();
     __builtin_amdgcn_wave_barrier();
-    for (int64_t g = flushed + 16 * lane; g < upto; g += 16 * 64) {
+    for (int32_t g = flushed + 16 * lane; g < upto; g += 16 * 64) {
       const u32x4_t v = *(const PQG_L u32x4_t*)(lds_ptr(sh->ring) + (g & (kRing - 1)));
       stg16((uintptr_t)(dst + g), make_uint4(v.x, v.y, v.z, v.w));
     }
     flushed = upto;
   }
   __device__ __forceinline__ void maybe_flush() {
-    const int64_t a = d & ~(int64_t)15;
+    const int32_t a = d & ~15;
     if (a - flushed >= kSnFlush) flush(a);
   }
 
   // A literal too long for one batch (or whose bytes leave the window):
   // pieces of up to kLongPiece bytes straight from the compressed block.
-  __device__ void long_literal(int64_t at, int64_t len) {
+  __device__ void long_literal(int32_t at, int32_t len) {
     const int lane = lane_id();
     constexpr int NG = kLongPiece / 1024;  // granules per lane
     while (len > 0) {
-      const int64_t a0 = d & ~(int64_t)15;
+      const int32_t a0 = d & ~15;
       const int pre = (int)(d - a0);
-      const int64_t piece = len < kLongPiece - pre ? len : kLongPiece - pre;
-      const int64_t lim = pre + piece;  // piece bytes are [pre, lim) of the granules from a0
+      const int32_t piece = len < kLongPiece - pre ? len : kLongPiece - pre;
+      const int32_t lim = pre + piece;  // piece bytes are [pre, lim) of the granules from a0
       uint4 x[NG], y[NG];
       uint32_t r[NG];
       bool nx[NG], ny[NG];
 #pragma unroll
       for (int j = 0; j < NG; j++) {
-        const int64_t i0 = 1024 * j + 16 * lane;  // granule's first byte (relative to a0)
-        const int64_t s0 = at + i0 - pre;         // block offset of that byte
+        const int32_t i0 = 1024 * j + 16 * lane;  // granule's first byte (relative to a0)
+        const int32_t s0 = at + i0 - pre;         // block offset of that byte
         const uintptr_t sa = (uintptr_t)(src + s0);
         r[j] = (uint32_t)(sa & 15);
-        const int64_t gb0 = s0 - (int64_t)r[j];   // aligned granule holding s0
+        const int32_t gb0 = s0 - (int32_t)r[j];   // aligned granule holding s0
         // load an aligned granule only if it holds a byte of the piece
-        const int64_t lo = at + (i0 > pre ? i0 - pre : 0), hi = at + (i0 + 16 < lim ? i0 + 16 : lim) - pre;
+        const int32_t lo = at + (i0 > pre ? i0 - pre : 0), hi = at + (i0 + 16 < lim ? i0 + 16 : lim) - pre;
         const bool need = i0 < lim && i0 + 16 > pre;
         // unconditional loads (a load under a branch is waited for inside it):
         // a granule not needed re-reads the literal's first one, zeroed below
@@ -386,8 +395,10 @@ struct SnapBlock {
 #endif
 #pragma unroll
       for (int j = 0; j < NG; j++) {
-        const int64_t i0 = 1024 * j + 16 * lane;
-        if (i0 >= lim) continue;
+        const int32_t i0 = 1024 * j + 16 * lane;
+        // (no early exit for lanes past the piece: every load is consumed on
+        // every path, or the wait analysis keeps it pending into the next
+        // tags and waits for all stores in flight there)
         const uint32_t q[8] = {x[j].x, x[j].y, x[j].z, x[j].w, y[j].x, y[j].y, y[j].z, y[j].w};
         const uint32_t qd = r[j] >> 2, sft = (r[j] & 3) * 8;
         uint32_t w[4];
@@ -413,7 +424,7 @@ struct SnapBlock {
             w[k] = (ow[k] & m) | (w[k] & ~m);
           }
         }
-        sts16(lds_ptr(sh->ring) + rp, make_uint4(w[0], w[1], w[2], w[3]));
+        if (i0 < lim) sts16(lds_ptr(sh->ring) + rp, make_uint4(w[0], w[1], w[2], w[3]));
       }
       __builtin_amdgcn_wave_barrier();
       d += piece;
@@ -424,9 +435,9 @@ struct SnapBlock {
   }
 
   // A literal of len bytes at window offset wo (len <= kWinLit, inside the window).
-  __device__ __forceinline__ void window_literal(uint32_t wo, int64_t len) {
+  __device__ __forceinline__ void window_literal(uint32_t wo, int32_t len) {
     const int lane = lane_id();
-    const int64_t a0 = d & ~(int64_t)15;
+    const int32_t a0 = d & ~15;
     const int pre = (int)(d - a0);
     const int lim = pre + (int)len;
     // A ragged first granule (pre > 0) is written byte by byte by lanes
@@ -456,25 +467,26 @@ struct SnapBlock {
   // Copy of len (<= 64) bytes from offset back, one byte per lane.
   __device__ __forceinline__ void copy_bytes(uint32_t off, int len) {
     const int lane = lane_id();
-    const int64_t ring_lo = ((d + 15) & ~(int64_t)15) - kRing;  // see below
+    const int32_t ring_lo = ((d + 15) & ~15) - kRing;  // see below
     int j = lane;
     if (off < (uint32_t)len) j = lane % (int)off;  // overlapping: the period of `off` bytes before d
-    const int64_t h = d - (int64_t)off + j;
-    if ((int64_t)(d - off) >= ring_lo) {
+    const int32_t h = d - (int32_t)off + j;          // (off <= d - base: checked by the callers)
+    if (d - (int32_t)off >= ring_lo) {
       const uint8_t b = lds_ptr(sh->ring)[(uint32_t)h & (kRing - 1)];
       if (lane < len) lds_ptr(sh->ring)[(uint32_t)(d + lane) & (kRing - 1)] = b;
     } else {
       // older than the ring (copy-4): the flushed output through L2, once the
       // flush stores have landed and this CU's L1 holds no stale line
       // (off > kRing - 16 > len: no overlap)
-      flush(d & ~(int64_t)15);
+      flush(d & ~15);
       __builtin_amdgcn_s_waitcnt(0);  // this wave's flush stores have reached L2
-      uint8_t b = 0;
-      if (lane < len) {
-        const uintptr_t a = (uintptr_t)(dst + h);
-        b = (uint8_t)(ld_l2_u32((const PQG_G uint32_t*)(a & ~(uintptr_t)3)) >> ((a & 3) * 8));
-      }
-      if (lane < len) lds_ptr(sh->ring)[(uint32_t)(d + lane) & (kRing - 1)] = b;
+      // every lane loads (h < d for all 64: off > 64), so that no load is
+      // left pending on a path the compiler cannot rule out (it would then
+      // wait for every store in flight at the next write of that register)
+      const uintptr_t a = (uintptr_t)(dst + h);
+      const uint32_t bw = ld_l2_u32((const PQG_G uint32_t*)(a & ~(uintptr_t)3)) >> ((a & 3) * 8);
+      asm volatile("" ::"v"(bw));  // consumed here, on every path
+      if (lane < len) lds_ptr(sh->ring)[(uint32_t)(d + lane) & (kRing - 1)] = (uint8_t)bw;
     }
     d += len;
   }
@@ -484,7 +496,7 @@ struct SnapBlock {
   struct Peek {
     uint32_t a, b, c, sft;
   };
-  __device__ __forceinline__ Peek peek_issue(int64_t t) {
+  __device__ __forceinline__ Peek peek_issue(int32_t t) {
     const uint32_t o = (uint32_t)(t - in_base);
     const PQG_L uint32_t* q = (const PQG_L uint32_t*)(lds_ptr(sh->in) + (o & ~3u));
     return Peek{q[0], q[1], q[2], (o & 3) * 8};
@@ -494,7 +506,7 @@ struct SnapBlock {
     return (uint64_t)__builtin_amdgcn_readfirstlane(lo) | (uint64_t)__builtin_amdgcn_readfirstlane(hi) << 32;
   }
   // 8 bytes at block offset t (inside the window): one broadcast LDS load
-  __device__ __forceinline__ uint64_t peek8(int64_t t) {
+  __device__ __forceinline__ uint64_t peek8(int32_t t) {
     const uint32_t o = (uint32_t)(t - in_base);
     const PQG_L uint32_t* q = (const PQG_L uint32_t*)(lds_ptr(sh->in) + (o & ~3u));
     const uint32_t a = q[0], b = q[1], c = q[2];
@@ -507,13 +519,19 @@ struct SnapBlock {
   // next tag's header read ahead of the current tag's bytes.  Returns to the
   // windowed resolution after a streak of short tags or at a window refill.
   // kOK, or kSNAPPY at a corrupt tag.
-  __device__ int serial(int64_t& s, int max) {
+  __device__ int serial(int32_t& s, int max) {
+    // loads the dense path issued under one branch and consumed under another
+    // look pending here to the compiler's wait analysis, which would then wait
+    // for all stores in flight at every write of their registers: one real
+    // wait here instead
+    __builtin_amdgcn_s_waitcnt(0);
     int short_streak = 0;
     uint64_t x8 = peek8(s);
     const bool lastsub = dend == dlen;
     for (int n = 0; n < max && s < slen && short_streak < 4 && (lastsub || d < dend); n++) {
       const uint32_t tag = (uint32_t)x8 & 0xff;
-      int64_t length, ns;
+      int64_t length;  // (a literal's length field is 32 bits: up to 2^32)
+      int32_t ns;
       uint32_t offset = 0;
       const bool lit = (tag & 3) == 0;
       int hdr;
@@ -528,7 +546,7 @@ struct SnapBlock {
         }
         length = (int64_t)x + 1;
         if (length > dend - d || length > slen - (s + hdr)) return kSNAPPY;
-        ns = s + hdr + length;
+        ns = s + hdr + (int32_t)length;
       } else {
         hdr = (tag & 3) == 1 ? 2 : (tag & 3) == 2 ? 3 : 5;
         if (s + hdr > slen) return kSNAPPY;
@@ -551,9 +569,9 @@ struct SnapBlock {
       // waited for after them (one LDS round trip per tag, not two)
       const Peek nx = peek_issue(next_in ? ns : in_base);
       if (lit) {
-        const int64_t at = s + hdr;
-        if ((d & 15) + length <= kWinLit && at + length <= in_base + kSnWin) window_literal((uint32_t)(at - in_base), length);
-        else long_literal(at, length);
+        const int32_t at = s + hdr;
+        if ((d & 15) + length <= kWinLit && at + length <= in_base + kSnWin) window_literal((uint32_t)(at - in_base), (int32_t)length);
+        else long_literal(at, (int32_t)length);
       } else {
         copy_bytes(offset, (int)length);
       }
@@ -562,7 +580,7 @@ struct SnapBlock {
       if (!next_in) break;
       x8 = peek_finish(nx);
     }
-    if ((d & ~(int64_t)15) - flushed >= kSnFlush) flush(d & ~(int64_t)15);
+    if ((d & ~15) - flushed >= kSnFlush) flush(d & ~15);
     return kOK;
   }
 
@@ -570,7 +588,7 @@ struct SnapBlock {
   // The ring holds output [ring_lo, d), ring_lo = roundup16(d) - kRing: a
   // ragged last granule overwrites the slots of the kRing-older bytes just
   // above d.
-  __device__ int run(int64_t s) {
+  __device__ int run(int32_t s) {
     const int lane = lane_id();
     PQG_ST(t_run0);
     const PQG_L uint8_t* IN = lds_ptr(sh->in);
@@ -582,7 +600,7 @@ struct SnapBlock {
       PQG_SA(8, 1);
       if (s < in_base || s + kSnWinNeed > in_base + kSnWin) {
         // pending output goes out with the window loads: one wait covers both
-        if ((d & ~(int64_t)15) - flushed >= 2048) flush(d & ~(int64_t)15);
+        if ((d & ~15) - flushed >= 2048) flush(d & ~15);
         fill(s);
       }
       PQG_ST(tb);
@@ -597,7 +615,7 @@ struct SnapBlock {
       }
       // A batch: up to kBatchWin windows of kPos positions whose chain tags
       // fill <= kSpan output bytes, resolved together (step 4a).
-      const int64_t a0 = d & ~(int64_t)15;
+      const int32_t a0 = d & ~15;
       const int pre = (int)(d - a0);
       int filled = pre;  // batch bytes [0, filled) from a0: history prefix + the tags so far
       int ntag = 0, nwin = 0;
@@ -632,7 +650,7 @@ struct SnapBlock {
 #else
         chain_marks128(n0, n1, lds_ptr(sh->cflag), cm0, cm1);
 #endif
-        const int64_t lim64 = slen - s;
+        const int32_t lim64 = slen - s;
         const int lim = lim64 < kPos ? (int)lim64 : kPos;
         if (lim < 64) {
           cm0 &= (1ull << lim) - 1;
@@ -668,8 +686,8 @@ struct SnapBlock {
         if (cutpos == 0) {
           if (nwin > 0) break;  // the batch so far is resolved first
           // tag 0 alone is too long for a batch: a literal (copies are <= 64 bytes)
-          const int64_t l0 = readlane64(t0.len, 0);
-          const int64_t at0 = s + __builtin_amdgcn_readlane(t0.hdr, 0);
+          const int32_t l0 = (int32_t)readlane64(t0.len, 0);  // (checked: <= dend - d)
+          const int32_t at0 = s + __builtin_amdgcn_readlane(t0.hdr, 0);
           long_literal(at0, l0);
           s = at0 + l0;
           serial_next = 64;
@@ -679,15 +697,14 @@ struct SnapBlock {
         // ---- the chain's tags before cutpos; output [dcur, dcur + out)
         const bool b0 = on0 && lane < cutpos, b1 = on1 && 64 + lane < cutpos;
         const uint64_t bm0 = __ballot(b0), bm1 = __ballot(b1);
-        int64_t out, s1;
+        int32_t out, s1;  // (the chain's tags passed the checks: out <= kSpan)
         if (cutpos < kPos) {
           const int l = cutpos & 63;
-          out = cutpos < 64 ? (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(i0 - o0), l)
-                            : (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(i1 - o1), l);
+          out = cutpos < 64 ? __builtin_amdgcn_readlane((int)(i0 - o0), l) : __builtin_amdgcn_readlane((int)(i1 - o1), l);
           s1 = s + cutpos;
         } else {
-          out = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)i1, 63);
-          s1 = s + readlane64(last < 64 ? t0.next : t1.next, last & 63);
+          out = __builtin_amdgcn_readlane((int)i1, 63);
+          s1 = s + (int32_t)readlane64(last < 64 ? t0.next : t1.next, last & 63);
         }
         PQG_ST(td);
         PQG_SA(2, td - tc);
@@ -701,10 +718,10 @@ struct SnapBlock {
             const int l = __ffsll((long long)(hi ? m1 : m0)) - 1;
             if (hi) m1 &= m1 - 1;
             else m0 &= m0 - 1;
-            const int64_t len = readlane64(hi ? t1.len : t0.len, l);
+            const int32_t len = (int32_t)readlane64(hi ? t1.len : t0.len, l);
             const bool lit = __builtin_amdgcn_readlane((int)(hi ? t1.lit : t0.lit), l) != 0;
             if (lit) {
-              const int64_t at = s + (hi ? 64 : 0) + l + __builtin_amdgcn_readlane(hi ? t1.hdr : t0.hdr, l);
+              const int32_t at = s + (hi ? 64 : 0) + l + __builtin_amdgcn_readlane(hi ? t1.hdr : t0.hdr, l);
               if ((d & 15) + len <= kWinLit) window_literal((uint32_t)(at - in_base), len);
               else long_literal(at, len);
             } else {
@@ -713,7 +730,7 @@ struct SnapBlock {
             maybe_flush();
           }
           s = s1;
-          if ((d & ~(int64_t)15) - flushed >= kSnFlush) flush(d & ~(int64_t)15);
+          if ((d & ~15) - flushed >= kSnFlush) flush(d & ~15);
           serial_next = 64;  // a tag-sparse stretch: continue tag by tag
           PQG_ST(tsp);
           PQG_SA(3, tsp - td);
@@ -754,7 +771,7 @@ struct SnapBlock {
       PQG_SA(12, ntag);
       // ---- 4a. dense: per-byte sources for the granules from a0
       const int end = filled;  // batch bytes [pre, end)
-      const int64_t d1 = a0 + filled;
+      const int32_t d1 = a0 + filled;
       __builtin_amdgcn_wave_barrier();
       // tag of each of this lane's 16 bytes: running max of the marks, then
       // the exclusive max over the lanes before
@@ -789,7 +806,7 @@ struct SnapBlock {
       // latency runs under the pointer doubling.  Only this wave's flush
       // stores need to have landed; the previous batch's went out a batch ago,
       // and this batch's pending output is flushed after these loads.
-      const int64_t ring_lo = ((d + 15) & ~(int64_t)15) - kRing;
+      const int32_t ring_lo = ((d + 15) & ~15) - kRing;
       uint32_t fm = 0;  // bytes whose (terminal) source is far
 #pragma unroll
       for (int k = 0; k < 16; k++) fm |= (own[k] < pre && a0 + own[k] < ring_lo) ? 1u << k : 0u;
@@ -800,7 +817,7 @@ struct SnapBlock {
         __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
         for (int k = 0; k < 16; k++) {  // unconditional loads (non-far bytes read the output's first dword)
-          const int64_t h = (fm >> k) & 1 ? a0 + own[k] : 0;
+          const int32_t h = (fm >> k) & 1 ? a0 + own[k] : 0;
           fw[k] = ld_l2_u32((const PQG_G uint32_t*)((uintptr_t)(dst + h) & ~(uintptr_t)3));
         }
       }
@@ -845,7 +862,7 @@ struct SnapBlock {
 #pragma unroll
       for (int k = 0; k < 16; k++) {
         const int32_t v = own[k];
-        const int64_t h = a0 + v;
+        const int32_t h = a0 + v;
         const uint32_t off = v >= kSpan ? in_off + (uint32_t)(v - kSpan) : (uint32_t)(h & (kRing - 1));
         fm2 |= (v < kSpan && h < ring_lo && !((fm >> k) & 1)) ? 1u << k : 0u;
         bt[k] = shb[off];
@@ -859,7 +876,7 @@ struct SnapBlock {
         __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
         for (int k = 0; k < 16; k++) {
-          const int64_t h = (fm2 >> k) & 1 ? a0 + own[k] : 0;
+          const int32_t h = (fm2 >> k) & 1 ? a0 + own[k] : 0;
           fw[k] = ld_l2_u32((const PQG_G uint32_t*)((uintptr_t)(dst + h) & ~(uintptr_t)3));
         }
 #pragma unroll
@@ -881,7 +898,7 @@ struct SnapBlock {
     PQG_ST(t_run1);
     PQG_SA(15, t_run1 - t_run0);
     if (d != dend) return kSNAPPY;
-    flush((dend + 15) & ~(int64_t)15);
+    flush((dend + 15) & ~15);
     return kOK;
   }
 
@@ -889,7 +906,7 @@ struct SnapBlock {
   // `target`, without producing output: the start of a sub-block found from a
   // chain tag before it.  kSNAPPY if a tag straddles target or the chain
   // leaves the block.
-  __device__ int skip_to(int64_t& s, int64_t target) {
+  __device__ int skip_to(int32_t& s, int32_t target) {
     const int lane = lane_id();
     const PQG_L uint8_t* IN = lds_ptr(sh->in);
     while (d < target) {
@@ -901,7 +918,7 @@ struct SnapBlock {
       const uint32_t n0 = (uint32_t)(t0.next < kPos ? t0.next : kPos), n1 = (uint32_t)(t1.next < kPos ? t1.next : kPos);
       const uint32_t l0 = (uint32_t)(t0.len < (1 << 30) ? t0.len : (1 << 30)),
                      l1 = (uint32_t)(t1.len < (1 << 30) ? t1.len : (1 << 30));
-      const int64_t lim64 = slen - s;
+      const int32_t lim64 = slen - s;
       const int lim = lim64 < kPos ? (int)lim64 : kPos;
       int p = 0;
       while (p < lim && d < target) {
@@ -1193,11 +1210,15 @@ __global__ void __launch_bounds__(64, PQG_SNAPPY_WPE) k_snap_decode(const JobDev
     if (pg.sn_fallback || sb.pos < 0) continue;
     const JobDev job = jobs[pg.job];
     const SnapLoc L = snap_loc(pg);
-    SnapBlock blk{gconst(job.data) + L.src_off, L.clen, gmut(scratch) + job.scratch_base + pg.scratch_offset, L.ulen,
-                  &sh};
-    blk.base = (int64_t)sb.j * kSnapSub;
-    blk.dend = blk.base + kSnapSub < L.ulen ? blk.base + kSnapSub : L.ulen;
-    int64_t s = sb.pos;
+    if (L.clen > kSnMaxLen || L.ulen > kSnMaxLen) {  // the serial path reports it
+      if (lane == 0) atomicOr(&pages[sb.page].sn_fallback, 64);
+      continue;
+    }
+    SnapBlock blk{gconst(job.data) + L.src_off, (int32_t)L.clen, gmut(scratch) + job.scratch_base + pg.scratch_offset,
+                  (int32_t)L.ulen, &sh};
+    blk.base = sb.j * kSnapSub;
+    blk.dend = (int64_t)blk.base + kSnapSub < L.ulen ? blk.base + kSnapSub : (int32_t)L.ulen;
+    int32_t s = sb.pos;
     blk.d = sb.out;
     int e = blk.d < blk.base ? blk.skip_to(s, blk.base) : (blk.d == blk.base ? kOK : kSNAPPY);
     int why = e != kOK ? 64 : 0;
@@ -1228,8 +1249,12 @@ __global__ void __launch_bounds__(64, PQG_SNAPPY_WPE) k_snappy(JobDev* jobs, Pag
     const SnapLoc L = snap_loc(pg);
     const JobDev job = jobs[pg.job];
     if (job.codec != kCodecSnappy) continue;
-    SnapBlock blk{gconst(job.data) + L.src_off, L.clen, gmut(scratch) + job.scratch_base + pg.scratch_offset, L.ulen,
-                  &sh};
+    if (L.clen > kSnMaxLen || L.ulen > kSnMaxLen) {  // beyond SnapBlock's 32-bit offsets
+      if (lane == 0) pages[pidx].read_status = kUNSUPPORTED;
+      continue;
+    }
+    SnapBlock blk{gconst(job.data) + L.src_off, (int32_t)L.clen, gmut(scratch) + job.scratch_base + pg.scratch_offset,
+                  (int32_t)L.ulen, &sh};
     int hl = 0;
     blk.fill(0);
     int e = snappy_header([&](int i) { return (int)lds_ptr(sh.in)[i - blk.in_base]; }, L.clen, L.ulen, &hl);

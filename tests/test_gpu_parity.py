@@ -555,3 +555,46 @@ def test_byte_array_chain_guesses_wrong(dec):
         b = bytearray(data)
         b[at] = val
         P.compare_file(bytes(b), dec)
+
+
+def test_delta_block_lengths_vary(dec):
+    """The speculative DBP header walk (pqg_values.hip dbp_decode): stretches of
+    equal-length blocks broken by blocks of other widths and other min-delta
+    varint lengths, and a ragged last block."""
+    rng = np.random.default_rng(11)
+    parts = []
+    for k, (nb, lo, hi) in enumerate([(40, 950, 1051), (3, 0, 1 << 20), (1, -5, 6), (70, 950, 1051), (2, 10**6, 10**6 + 3),
+                                      (1, -(1 << 40), 1 << 40), (30, 950, 1051)]):
+        parts.append(rng.integers(lo, hi, size=nb * 128 + (k == 6) * 57, dtype=np.int64))
+    v = np.cumsum(np.concatenate(parts))
+    for codec, ver in ((W.UNCOMPRESSED, 1), (W.SNAPPY, 2)):
+        data = W.write_file([W.Column("d", W.INT64, v, encoding=W.DELTA_BINARY_PACKED, rows_per_page=len(v),
+                                      codec=codec, page_version=ver)], len(v))
+        P.compare_file(data, dec)
+        v32 = (v & 0x7FFFFFFF).astype(np.int32)
+        data = W.write_file([W.Column("d", W.INT32, v32, encoding=W.DELTA_BINARY_PACKED, rows_per_page=len(v32),
+                                      codec=codec, page_version=ver)], len(v32))
+        P.compare_file(data, dec)
+
+
+def test_delta_corrupt_bytes_match(dec):
+    """One byte of a DBP page's block headers overwritten — a width past the
+    type's bits (0x41, 0xFF), a width that changes the block's length (8, 0),
+    a min delta one varint byte longer — at blocks inside and at the edges of
+    the speculative walk's 64-header groups: GPU and oracle agree on the
+    status and on every value."""
+    rng = np.random.default_rng(12)
+    v = np.cumsum(1000 + rng.integers(-50, 51, size=150 * 128, dtype=np.int64))
+    base = W.write_file([W.Column("d", W.INT64, v, encoding=W.DELTA_BINARY_PACKED, rows_per_page=len(v))], len(v))
+    # every block here is [2-byte min delta][widths 7 7 7 7][4 x 28 bytes]
+    at = [i for i in range(len(base) - 3) if base[i:i + 4] == b"\x07\x07\x07\x07"]
+    heads = [a for a, b in zip(at, at[1:]) if b - a == 118] + [at[-1]]
+    assert len(heads) >= 140
+    statuses = set()
+    for blk in (1, 2, 37, 63, 64, 65, 100, 127, 128, len(heads) - 1):
+        w = heads[blk]
+        for pos, byte in ((w + 1, 0x41), (w + 3, 0xFF), (w, 8), (w + 2, 0), (w - 2, base[w - 2] | 0x80)):
+            data = bytearray(base)
+            data[pos] = byte
+            statuses.add(P.compare_file(bytes(data), dec)[0].status)
+    assert len(statuses) > 1  # errors were reached, not only silent value changes
