@@ -191,7 +191,8 @@ struct JobDev {
   // ---- K1 speculative page scan (see k_page_cands / k_page_chain)
   int64_t tile_base;       // first scan tile of this job (global tile index)
   int32_t n_tiles;         // ceil(min(tcs, data_len) / kScanTile)
-  int32_t scan_fallback;   // 1: the serial walk (k_scan_pages) decodes this job's page list
+  int32_t scan_fallback;   // 1: the serial walk (k_scan_pages) decodes this job's page list;
+                           // 2: walked before the candidate scan (a few big pages)
   int32_t n_cands;         // header candidates found in the job's bytes
   int32_t n_ok;            // candidates whose read phase succeeds
   int32_t brk;             // first ok-rank whose successor is not the next ok candidate
@@ -295,6 +296,7 @@ constexpr int kQueueSlots = 15;  // queue regions zeroed per launch: 0-8, the st
 
 // Scan tiles of the speculative page-header search.
 constexpr int kScanTile = 16384;
+constexpr int kPrewalkPages = 4;  // K1: chunks of <= this many big pages are walked, not scanned
 constexpr int kCandPerTile = 64;
 
 // A page-header candidate: a position whose bytes parse as a PageHeader

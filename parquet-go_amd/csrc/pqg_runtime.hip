@@ -39,7 +39,7 @@ __global__ void k_cand_link(JobDev* jobs, const int* tile_job, int64_t total_til
                             int* ok2slot);
 __global__ void k_page_chain(JobDev* jobs, PageDev* pages, const Cand* cands, const int* succ,
                              const int* idx2slot, const int* ok2slot, int* order);
-__global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs);
+__global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs, int prewalk);
 __global__ void k_page_list(JobDev* jobs, PageDev* pages, int n_jobs, int* list, int list_cap, int* total,
                             int* queues);
 __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
@@ -501,6 +501,9 @@ static int launch_pipeline(pqg_ctx* c) {
   Cand* cands = (Cand*)c->cands.p;
   int* tokc = (int*)c->tile_okc.p;
   int* tokoff = (int*)c->tile_okoff.p;
+  // chunks of a few big pages (parquet-go's writer layout) are walked first
+  // and skipped by the candidate scan
+  hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n, kPrewalkPages);
   if (nt > 0) {
     int64_t* cpos = (int64_t*)c->cand_pos.p;
     int* clist = (int*)c->cand_list.p;
@@ -519,7 +522,7 @@ static int launch_pipeline(pqg_ctx* c) {
                        tcount, toff, tokoff, cands, (int*)c->succ.p, (int*)c->idx2slot.p, (int*)c->ok2slot.p);
   hipLaunchKernelGGL(k_page_chain, dim3(n), dim3(1024), 0, s, jobs, pages, cands, (const int*)c->succ.p,
                      (const int*)c->idx2slot.p, (const int*)c->ok2slot.p, (int*)c->order.p);
-  hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n);
+  hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n, 0);
   if (c->timed) hipEventRecord(c->ev[1], s);
   hipLaunchKernelGGL(k_page_list, dim3(n), dim3(1024), 0, s, jobs, pages, n, list,
                      (int)std::min<int64_t>(c->list_cap, INT32_MAX), ctr, ctr + 8);

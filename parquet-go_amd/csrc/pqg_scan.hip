@@ -299,6 +299,13 @@ __global__ void __launch_bounds__(256) k_page_cands(JobDev* jobs, const int* til
   }
   __syncthreads();
   const JobDev& job = jobs[job_s];
+  if (job.scan_fallback == 2) {  // walked before the scan: no candidates
+    if (tid == 0) {
+      tile_count[tile] = 0;
+      tile_okc[tile] = 0;
+    }
+    return;
+  }
   const int64_t lim = job.tcs < job.data_len ? job.tcs : job.data_len;
   const int64_t t0 = (tile - job.tile_base) * kScanTile;
   const int64_t t1 = t0 + kScanTile < lim ? t0 + kScanTile : lim;
@@ -407,6 +414,7 @@ __global__ void __launch_bounds__(1024) k_tile_scan(JobDev* jobs, const int* til
   __shared__ int ovf;
   JobDev& job = jobs[blockIdx.x];
   const int tid = threadIdx.x;
+  if (job.scan_fallback == 2) return;  // walked before the scan (k_scan_pages prewalk)
   if (tid == 0) ovf = 0;
   __syncthreads();
   const int nt = job.n_tiles;
@@ -686,12 +694,58 @@ struct ScanShared {
   int16_t last[kMaxLast];
 };
 
-__global__ void __launch_bounds__(64) k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs) {
+// prewalk > 0: before the candidate scan, chunks of at most `prewalk` big
+// pages (each data page >= 1/8 of the chunk: parquet-go's writer puts a whole
+// chunk in one page) are walked here, and their bytes are not scanned
+// (scan_fallback = 2 tells K1a-K1d to skip the job).  A headers-only walk
+// decides; only a walk that reaches the chunk's end (or its first failing
+// page) within the limit is redone with its page records.  prewalk == 0: the
+// jobs the speculative path could not settle (scan_fallback == 1).
+__global__ void __launch_bounds__(64) k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs, int prewalk) {
   __shared__ __attribute__((aligned(16))) ScanShared sh;
   int j = blockIdx.x;
   if (j >= n_jobs) return;
   JobDev& job = jobs[j];
-  if (!job.scan_fallback) return;
+  const int64_t tcs = job.tcs;
+  if (prewalk > 0) {
+    if (job.scan_fallback || tcs <= 0) return;
+    Window win{gconst(job.data), job.data_len, kFarAway, lds_ptr(sh.win)};
+    int64_t pos = 0;
+    bool dict_seen = false, done = false;
+    for (int np = 0;; np++) {
+      if (tcs - pos <= 0) {
+        done = true;
+        break;
+      }
+      if (np == prewalk) break;
+      Compact<WinSrc> c;
+      c.src.w = win;
+      c.pos = pos;
+      c.frames = sh.frames;
+      c.last = sh.last;
+      c.nlast = 0;
+      c.last_id = 0;
+      c.bool_set = false;
+      c.bool_val = false;
+      PageHdr h;
+      int e = c.read_page_header(&h);
+      win = c.src.w;
+      PageDev pg;
+      init_page(pg, j, pos, c.pos);
+      int64_t next, comp;
+      e = classify_page(job, h, e, c.pos, dict_seen, pg, &next, &comp);
+      if (e != kOK) {
+        done = true;
+        break;
+      }
+      if (h.type != 2 && next - pos < tcs / 8) break;  // small pages: many of them, the candidate scan
+      if (h.type == 2) dict_seen = true;
+      pos = next;
+    }
+    if (!done) return;
+  } else if (job.scan_fallback != 1) {
+    return;
+  }
   Window win{gconst(job.data), job.data_len, kFarAway, lds_ptr(sh.win)};
   int64_t pos = 0;
   int np = 0;
@@ -701,7 +755,6 @@ __global__ void __launch_bounds__(64) k_scan_pages(JobDev* jobs, PageDev* pages,
   int64_t scratch = 0;
   int64_t slots = 0;
   const int lane = lane_id();
-  const int64_t tcs = job.tcs;
   while (tcs - pos > 0) {
     Compact<WinSrc> c;
     c.src.w = win;
@@ -740,6 +793,7 @@ __global__ void __launch_bounds__(64) k_scan_pages(JobDev* jobs, PageDev* pages,
   }
   if (lane == 0) {
     init_job_results(job);
+    if (prewalk > 0) job.scan_fallback = 2;
     job.num_pages = np;
     job.dict_page = dict_page;
     job.scan_status = status;

@@ -308,7 +308,7 @@ struct SnapBlock {
   int32_t base = 0;
   int32_t dend = -1;
 #ifdef PQG_PROFILE
-  uint64_t pacc[16] = {0};
+  uint64_t pacc[24] = {0};
 #define PQG_ST(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define PQG_SA(k, x) pacc[k] += (x)
 #else
@@ -529,6 +529,8 @@ struct SnapBlock {
     uint64_t x8 = peek8(s);
     const bool lastsub = dend == dlen;
     for (int n = 0; n < max && s < slen && short_streak < 4 && (lastsub || d < dend); n++) {
+      PQG_ST(q0);
+      PQG_SA(21, 1);
       const uint32_t tag = (uint32_t)x8 & 0xff;
       int64_t length;  // (a literal's length field is 32 bits: up to 2^32)
       int32_t ns;
@@ -568,6 +570,8 @@ struct SnapBlock {
       // the next header's loads go out ahead of this tag's bytes and are
       // waited for after them (one LDS round trip per tag, not two)
       const Peek nx = peek_issue(next_in ? ns : in_base);
+      PQG_ST(q1);
+      PQG_SA(16, q1 - q0);
       if (lit) {
         const int32_t at = s + hdr;
         if ((d & 15) + length <= kWinLit && at + length <= in_base + kSnWin) window_literal((uint32_t)(at - in_base), (int32_t)length);
@@ -575,10 +579,16 @@ struct SnapBlock {
       } else {
         copy_bytes(offset, (int)length);
       }
+      PQG_ST(q2);
+      PQG_SA(lit ? 17 : 18, q2 - q1);
       maybe_flush();  // keeps the unflushed tail inside the ring
+      PQG_ST(q3);
+      PQG_SA(19, q3 - q2);
       s = ns;
       if (!next_in) break;
       x8 = peek_finish(nx);
+      PQG_ST(q4);
+      PQG_SA(20, q4 - q3);
     }
     if ((d & ~15) - flushed >= kSnFlush) flush(d & ~15);
     return kOK;
@@ -1228,7 +1238,7 @@ __global__ void __launch_bounds__(64, PQG_SNAPPY_WPE) k_snap_decode(const JobDev
       if (e != kOK) why = 128;
     }
 #ifdef PQG_PROFILE
-    for (int k = 0; k < 16; k++) PQG_ACC(k, 0, blk.pacc[k]);
+    for (int k = 0; k < 24; k++) PQG_ACC(k, 0, blk.pacc[k]);
 #endif
     if (why && lane == 0) atomicOr(&pages[sb.page].sn_fallback, why);
   }
@@ -1260,7 +1270,7 @@ __global__ void __launch_bounds__(64, PQG_SNAPPY_WPE) k_snappy(JobDev* jobs, Pag
     int e = snappy_header([&](int i) { return (int)lds_ptr(sh.in)[i - blk.in_base]; }, L.clen, L.ulen, &hl);
     if (e == kOK) e = blk.run(hl);
 #ifdef PQG_PROFILE
-    for (int k = 0; k < 16; k++) PQG_ACC(k, 0, blk.pacc[k]);
+    for (int k = 0; k < 24; k++) PQG_ACC(k, 0, blk.pacc[k]);
 #endif
     // V1: getValuesDecoder runs after the block is decompressed (page_v1.go:91-97)
     if (e == kOK && pg.page_type == 0 && !values_supported(job.type, job.type_length, pg.encoding)) e = kUNSUPPORTED;

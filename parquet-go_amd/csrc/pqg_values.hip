@@ -423,15 +423,29 @@ __device__ __forceinline__ uint64_t dbp_tile(const DbpShared& sh, const PQG_L ui
   const uint64_t mnd = S->mind[b];
   const uint64_t wmask = wv == 64 ? ~0ull : ((1ull << wv) - 1);  // wv == 0: 0
   uint64_t d[4], local = 0;
+  if (!__ballot(wv > 32)) {
+    // widths <= 32 (every INT32 page, most INT64 ones): a value's bits lie in
+    // two dwords, so two LDS reads per value instead of three
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const uint32_t bt = bit0 + (uint32_t)(k * wv);
-    const uint32_t dw = bt >> 5, sh5 = bt & 31;
-    const uint64_t lo = (uint64_t)stw[dw] | ((uint64_t)stw[dw + 1] << 32);
-    const uint64_t x = (lo >> sh5) | (((uint64_t)stw[dw + 2] << (63 - sh5)) << 1);
-    const uint64_t dv = (x & wmask) + mnd;
-    d[k] = Full || k < nvp ? dv : 0;
-    local += d[k];
+    for (int k = 0; k < 4; k++) {
+      const uint32_t bt = bit0 + (uint32_t)(k * wv);
+      const uint32_t dw = bt >> 5, sh5 = bt & 31;
+      const uint64_t lo = (uint64_t)stw[dw] | ((uint64_t)stw[dw + 1] << 32);
+      const uint64_t dv = ((lo >> sh5) & wmask) + mnd;
+      d[k] = Full || k < nvp ? dv : 0;
+      local += d[k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t bt = bit0 + (uint32_t)(k * wv);
+      const uint32_t dw = bt >> 5, sh5 = bt & 31;
+      const uint64_t lo = (uint64_t)stw[dw] | ((uint64_t)stw[dw + 1] << 32);
+      const uint64_t x = (lo >> sh5) | (((uint64_t)stw[dw + 2] << (63 - sh5)) << 1);
+      const uint64_t dv = (x & wmask) + mnd;
+      d[k] = Full || k < nvp ? dv : 0;
+      local += d[k];
+    }
   }
   const uint64_t incl = wave_incl_scan_u64(local);
   uint64_t run = carry + (incl - local);

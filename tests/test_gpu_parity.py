@@ -320,6 +320,25 @@ def test_scan_speculative_path_used(dec):
     assert walk == 0 and pages == 5 and scratch > 0
 
 
+def test_scan_big_pages_prewalked(dec):
+    # a chunk of <= 4 big pages (parquet-go's writer: one page per chunk) is
+    # walked before the candidate scan (serial_walk == 2) and skipped by it
+    data, _ = W.config_c1(rows=100_003, rows_per_page=100_003)
+    walk, cands, pages, _ = _decode_one(dec, data)
+    assert walk == 2 and pages == 1 and cands == 0
+    data = W.config_c4(rows=40_000, vocab=3000, rows_per_page=40_000, codec=W.UNCOMPRESSED)[0]
+    walk, _, pages, _ = _decode_one(dec, data)
+    assert walk == 2 and pages == 2  # dictionary page + one data page
+    data, _ = W.config_c1(rows=40_000, rows_per_page=10_000)  # 4 pages of 1/4: walked
+    walk, _, pages, _ = _decode_one(dec, data)
+    assert walk == 2 and pages == 4
+    # an understated TotalCompressedSize / a damaged big page: still the oracle's result
+    data, _ = W.config_c1(rows=100_003, rows_per_page=100_003)
+    b = bytearray(data)
+    b[6] ^= 0xFF
+    P.compare_file(bytes(b), dec)
+
+
 def test_scan_false_candidates_are_skipped(dec):
     # PLAIN int32 payload bytes 15 00 15 00 parse as page-header prefixes: a few
     # per tile are false candidates the chain must jump over
