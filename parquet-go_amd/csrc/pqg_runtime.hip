@@ -193,6 +193,11 @@ struct pqg_ctx {
   std::vector<JobDev> plan;             // per-job capacities used
   std::vector<Caps> force;              // per-job capacities forced for this batch
   std::map<JobKey, Caps> learned;       // grown capacities, across calls
+  // chunks seen with more pages than the K1 prewalk takes: a batch of only
+  // such chunks skips the prewalk launch (performance only: the candidate
+  // scan settles any chunk, so a stale entry never changes a result)
+  std::map<JobKey, bool> many_pages;
+  bool prewalk = true;
   int launches = 0;                     // pipeline launches of the last decode
   bool any_var = false;                 // batch holds variable-length columns
   bool any_fixed_other = false;         // batch holds fixed-width columns (k_values<0> pages possible)
@@ -503,7 +508,7 @@ static int launch_pipeline(pqg_ctx* c) {
   int* tokoff = (int*)c->tile_okoff.p;
   // chunks of a few big pages (parquet-go's writer layout) are walked first
   // and skipped by the candidate scan
-  hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n, kPrewalkPages);
+  if (c->prewalk) hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n, kPrewalkPages);
   if (nt > 0) {
     int64_t* cpos = (int64_t*)c->cand_pos.p;
     int* clist = (int*)c->cand_list.p;
@@ -621,9 +626,12 @@ int pqg_decode_chunks_async(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs) {
   c->force.assign((size_t)n_jobs, Caps());
   c->any_var = false;
   c->any_fixed_other = false;
+  c->prewalk = false;
   for (int i = 0; i < n_jobs; i++) {
-    auto it = c->learned.find(JobKey{(uintptr_t)jobs[i].data, jobs[i].total_compressed_size, jobs[i].num_values_hint});
+    const JobKey key{(uintptr_t)jobs[i].data, jobs[i].total_compressed_size, jobs[i].num_values_hint};
+    auto it = c->learned.find(key);
     if (it != c->learned.end()) c->force[(size_t)i] = it->second;
+    c->prewalk |= c->many_pages.find(key) == c->many_pages.end();
     // the strings stage: variable-length columns, and FLBA (DELTA_BYTE_ARRAY pages)
     c->any_var |= value_width_of(jobs[i].col) == 0 || jobs[i].col.physical_type == PQG_FIXED_LEN_BYTE_ARRAY;
     // k_values<0>: every fixed-width column but 4-byte ones with only dictionary pages
@@ -678,6 +686,11 @@ int pqg_sync(pqg_ctx* c, pqg_chunk_result* results, int n_jobs) {
   }
   for (int i = 0; i < n; i++) {
     const JobDev& d = c->h_jobs[i];
+    if (d.status != PQG_ERR_CAPACITY && d.num_pages > kPrewalkPages) {
+      if (c->many_pages.size() >= 65536) c->many_pages.clear();  // bounded: a cache, not a record
+      const pqg_chunk_job& in = c->cur[(size_t)i];
+      c->many_pages[JobKey{(uintptr_t)in.data, in.total_compressed_size, in.num_values_hint}] = true;
+    }
     pqg_chunk_result& r = results[i];
     memset(&r, 0, sizeof(r));
     r.status = d.status;
