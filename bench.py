@@ -43,7 +43,7 @@ for p in (ROOT, os.path.join(ROOT, "parquet-go_amd")):
 METRIC = "decoded GB/s (uncompressed output) per GPU & node at 1/2/4/8; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 STAGES = ["scan", "list", "snappy", "levels", "walk", "unused", "nn_scan", "values", "strings", "finalize"]
-PROFILE_TAG = "r04"
+PROFILE_TAG = "r05"
 
 
 def log(*a):
@@ -64,6 +64,11 @@ def host_cores():
         return int(share), "sched_getaffinity %d CPUs; capped at the box's per-GPU share OMP_NUM_THREADS=%s" % (
             aff, share)
     return max(1, aff), "sched_getaffinity %d CPUs" % aff
+
+
+def peak_rss_gb():
+    import resource
+    return round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6, 2)  # ru_maxrss: KiB on Linux
 
 
 # ---------------------------------------------------------------- workloads
@@ -196,14 +201,21 @@ def account(wl, dec, res):
 
 # ---------------------------------------------------------------- verification
 def verify(wl, dec, res):
+    """Every decoded chunk against the generator's arrays.  C5: the expected
+    arrays of one row group at a time (regenerated, then dropped), so a rank
+    holds its file plus one row group's arrays."""
     ok = True
     ji = 0
     for pf, specs, (kind, exp) in wl.files:
+        cur_rg, cur = None, None
         for (rg, col) in specs:
             r = res[ji]
             ji += 1
             if r.status != 0:
                 return False
+            if kind == "c5" and rg != cur_rg:
+                cur_rg, cur = rg, None
+                cur = exp["part"](rg)
             if kind == "c2":
                 defs, vals = exp
                 ok &= np.array_equal(dec.d2h(r.def_levels, r.num_slots), defs)
@@ -215,7 +227,7 @@ def verify(wl, dec, res):
                 ok &= np.array_equal(dec.d2h(r.offsets, (r.num_values + 1) * 8, np.int64), exp["offsets"])
                 ok &= np.array_equal(dec.d2h(r.values, r.values_bytes), exp["chars"])
             elif kind == "c5":
-                e = exp["parts"][rg][pf.columns[col].path.decode().split(".")[0]]
+                e = cur[pf.columns[col].path.decode().split(".")[0]]
                 if "offsets" in e:
                     ok &= np.array_equal(dec.d2h(r.offsets, (r.num_values + 1) * 8, np.int64), e["offsets"])
                 ok &= np.array_equal(dec.d2h(r.values, r.values_bytes), np.ascontiguousarray(e["values"]).view(np.uint8))
@@ -284,7 +296,7 @@ def cpu_baseline(wl, seconds):
 STAGE_KERNELS = {"scan": ["k_tile_jobs", "k_page_cands", "k_cand_parse", "k_tile_scan", "k_cand_link", "k_page_chain",
                           "k_scan_pages"], "list": ["k_page_list"], "snappy": ["k_snap_plan", "k_snap_seg", "k_snap_link", "k_snap_decode", "k_snappy"], "levels": ["k_page_levels"],
                  "walk": ["k_hybrid_walk"], "unused": [], "nn_scan": ["k_nn_scan"],
-                 "values": ["k_values", "k_dict4"], "strings": ["k_str_dict", "k_str_plain", "k_str_count", "k_char_scan",
+                 "values": ["k_values", "k_dict_plan", "k_dict4", "k_dict_walk"], "strings": ["k_str_dict", "k_str_plain", "k_str_count", "k_char_scan",
                                                   "k_str_copy"],
                  "finalize": ["k_finalize"]}
 
@@ -382,6 +394,7 @@ def run_workload(wl, dec, args, steps, warmup, barrier, dist, world, rank, cpu_s
         out["verified_bit_exact"] = verify(wl, dec, res)
         if not out["verified_bit_exact"]:
             log("VERIFY FAILED:", wl.key)
+    out["host_peak_rss_gb"] = peak_rss_gb()  # this rank, so far (generation, upload, verification)
     if rank == 0 and not args.no_cpu:
         single, pool = cpu_baseline(wl, cpu_seconds)
         out["cpu_baseline"] = single
@@ -449,7 +462,7 @@ def k8_list_c5(dec, wl, res, args):
             rows = a.num_rows
             ok &= rows == info["rows_per_rg"] and a.num_valid == r.num_values
             lo = dec.d2h(lop, (rows + 1) * 4, np.int32)
-            e = info["parts"][specs[i][0]]["lst"]
+            e = info["part"](specs[i][0])["lst"]
             starts = np.flatnonzero(e["rep_levels"] == 0)
             el = e["def_levels"] >= 2
             ok &= bool(np.array_equal(lo, np.r_[np.cumsum(el)[starts] - el[starts], el.sum()].astype(np.int32)))

@@ -435,4 +435,12 @@ def config_c5(row_groups=(0,), rows_per_rg=C5_ROWS_PER_RG, seed=5, rows_per_page
         Column("i64s", INT64, cat("i64s", "values"), codec=SNAPPY, rows_per_page=rows_per_page),
     ]
     data = write_file(cols, rows, row_groups=len(parts))
-    return data, {"rows": rows, "row_groups": list(row_groups), "rows_per_rg": rows_per_rg, "parts": parts}
+    del cols, parts
+    rgs = list(row_groups)
+
+    def part(i):
+        """Expected arrays of the file's row group i, regenerated (the same seeds):
+        callers hold one row group's arrays at a time."""
+        return c5_row_group_columns(rgs[i], rows_per_rg, seed, rows_per_page)
+
+    return data, {"rows": rows, "row_groups": rgs, "rows_per_rg": rows_per_rg, "part": part}

@@ -44,6 +44,7 @@ def lib():
         L.pqo_gzip_decode.argtypes = [C.c_char_p, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
         L.pqo_delta_decode64.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_void_p]
         L.pqo_delta_decode32.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_void_p]
+        L.pqo_delta_lengths_end.argtypes = [C.c_char_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
         L.pqo_assemble.argtypes = [C.POINTER(abi.AssembleArgs)]
         L.pqo_assemble_list.argtypes = [C.POINTER(abi.ListArgs)]
         L.pqo_decode_column_store.argtypes = [C.POINTER(abi.ChunkJob), C.c_int, C.c_int, C.POINTER(StoreRG)]
@@ -88,6 +89,14 @@ def delta_decode(buf: bytes, count: int, bits: int = 64):
     fn = lib().pqo_delta_decode64 if bits == 64 else lib().pqo_delta_decode32
     rc = fn(bytes(buf), len(buf), count, out.ctypes.data)
     return rc, out[:count]
+
+
+def delta_lengths_end(buf: bytes, keep: int):
+    """(status, reader end, valuesCount) of a DBP length stream: `keep`
+    values decoded one by one, the rest skipped (DeltaBP::skip_rest)."""
+    end, cnt = C.c_int64(0), C.c_int64(0)
+    rc = lib().pqo_delta_lengths_end(bytes(buf), len(buf), keep, C.byref(end), C.byref(cnt))
+    return rc, end.value, cnt.value
 
 
 class OracleChunk:

@@ -229,6 +229,7 @@ constexpr int kCtrItems = 48;     // values-stage parts of the batch
 constexpr int kCtrLongLev = 49;   // long level runs
 constexpr int kCtrLevPieces = 50; // pieces of the long level runs
 constexpr int kCtrLongWalk = 51;  // long bit-packed runs of value streams
+constexpr int kCtrPartsCap = 52;  // the parts table's capacity (k_nn_scan): consumers read min(items, this)
 
 struct PartRec {
   int32_t pidx;    // PageDev index
@@ -292,7 +293,9 @@ constexpr int kQueueStrDelta = 11;
 constexpr int kQueueStrDba = 12;
 constexpr int kQueueLevLong = 13;  // pieces of the long level runs (k_level_long)
 constexpr int kQueueInflate = 14;  // GZIP pages (k_inflate)
-constexpr int kQueueSlots = 15;  // queue regions zeroed per launch: 0-8, the stage flags (9), 10-14
+constexpr int kQueueDictWalk = 15;   // small 4-byte dictionary pages walked in-kernel, LDS dictionary (k_dict_walk)
+constexpr int kQueueDictWalkG = 16;  // the same, dictionary gathered from global memory (k_dict_walk_g)
+constexpr int kQueueSlots = 17;  // queue regions zeroed per launch: 0-8, the stage flags (9), 10-16
 
 // Scan tiles of the speculative page-header search.
 constexpr int kScanTile = 16384;

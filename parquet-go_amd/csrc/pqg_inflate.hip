@@ -473,14 +473,18 @@ struct Inflater {
         for (uint32_t k = 0; k < xlen; k++)
           if (!hbyte(&v)) return kGZIP;
       }
+      // FNAME, FCOMMENT: Go's readString reads into a [512]byte buffer, so the
+      // NUL must come within 512 bytes (ErrHeader otherwise)
       if (flg & 8) {  // FNAME
+        uint32_t k = 0;
         do {
-          if (!hbyte(&v)) return kGZIP;
+          if (k++ == 512 || !hbyte(&v)) return kGZIP;
         } while (v != 0);
       }
       if (flg & 16) {  // FCOMMENT
+        uint32_t k = 0;
         do {
-          if (!hbyte(&v)) return kGZIP;
+          if (k++ == 512 || !hbyte(&v)) return kGZIP;
         } while (v != 0);
       }
       if (flg & 2) {  // FHCRC: the low 16 bits of the header's CRC-32

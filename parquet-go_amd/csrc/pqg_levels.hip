@@ -137,7 +137,7 @@ __device__ __forceinline__ void sync_ensure(LaneWin& w, bool reads, uint32_t rp)
 // [2 total, 3 total) the value streams, so a wave's lanes do alike work.
 __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pages, const int* list, const int* total,
                                                               HStream* streams, RunEnt* runs, BlockDesc* blks,
-                                                              LongWalk* longs, int long_cap) {
+                                                              LongWalk* longs, int long_cap, int skip_dict_small) {
   static_assert(kWalkThreads == 64, "LaneWin: dword k of lane L at buf[64 k + L]");
   __shared__ uint32_t buf[4 * kLaneWinG * kWalkThreads];  // each lane's 128-byte window (LaneWin)
   const int nt = *total;
@@ -147,7 +147,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pag
   for (int g = blockIdx.x * kWalkThreads + threadIdx.x; g < nt; g += gridDim.x * kWalkThreads) {
     const PageDev& pg = pages[list[g]];
     const int hs = pg.hs_val;
-    if (hs < 0) continue;
+    if (hs < 0 || (skip_dict_small && dict_walk_page(pg))) continue;  // k_dict4 walks those (IdxWalk)
     HStream& S = streams[hs];
     const uint32_t w = (uint32_t)S.w;
     const uint32_t n = (uint32_t)S.n, count = (uint32_t)S.count;
@@ -1285,7 +1285,7 @@ __global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, 
   int np = job.num_pages < job.page_cap ? job.num_pages : job.page_cap;
   if (job.status == kCAPACITY) np = 0;
   if (np <= kNnFastSeg * 1024) {
-    __shared__ int64_t s_base;
+    __shared__ int64_t s_base, s_res;
     __shared__ int s_big[256];
     __shared__ int64_t s_boff[256];
     __shared__ int s_nbig;
@@ -1350,8 +1350,13 @@ __global__ void __launch_bounds__(1024) k_nn_scan(JobDev* jobs, PageDev* pages, 
       s_base = base;
       s_cap = cap;
       s_nbig = 0;
+      s_res = fail0 ? 0 : ktot;  // reserved slots (even when they do not fit)
+      if (blockIdx.x == 0) ctr[kCtrPartsCap] = (int)(parts_cap < INT32_MAX ? parts_cap : INT32_MAX);
     }
     __syncthreads();
+    if (s_cap) {  // a reservation past the table: its slots inside the table hold no part
+      for (int64_t k = s_base + threadIdx.x; k < s_base + s_res && k < parts_cap; k += 1024) parts[k].vmode = -1;
+    }
     // value offsets (always: the later stages read them), then the parts
 #pragma unroll
     for (int j = 0; j < kNnFastSeg; j++)
@@ -1585,9 +1590,14 @@ __device__ void plan_parts(JobDev& job, int np, bool fail, const PageDev* pp, co
     job.item_base = base;
     job.n_items = s_fail ? 0 : (int32_t)tot;
     s_base = base;
+    if (blockIdx.x == 0) ctr[kCtrPartsCap] = (int)(cap < INT32_MAX ? cap : INT32_MAX);
   }
   __syncthreads();
-  if (s_fail) return;
+  if (s_fail) {  // a reservation past the table: its slots inside the table hold no part
+    if (!fail)
+      for (int64_t k = s_base + threadIdx.x; k < s_base + tot && k < cap; k += 1024) parts[k].vmode = -1;
+    return;
+  }
   plan_parts_from(job, np, pp, streams, blks, parts, s_base);
 }
 

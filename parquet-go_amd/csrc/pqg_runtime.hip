@@ -60,7 +60,7 @@ __global__ void k_page_levels(JobDev* jobs, PageDev* pages, const int* list, con
 __global__ void k_level_long(PageDev* pages, const int* ctr, const LongLev* longs, int long_cap,
                              const LevPiece* pieces, int piece_cap, int* queue);
 __global__ void k_hybrid_walk(const PageDev* pages, const int* list, const int* total, HStream* streams,
-                              RunEnt* runs, BlockDesc* blks, LongWalk* longs, int long_cap);
+                              RunEnt* runs, BlockDesc* blks, LongWalk* longs, int long_cap, int skip_dict_small);
 __global__ void k_walk_long(const int* ctr, const LongWalk* longs, int long_cap, BlockDesc* blks);
 __global__ void k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch, const HStream* streams, const BlockDesc* blks,
                           int* ctr, PartRec* parts, int64_t parts_cap);
@@ -69,8 +69,10 @@ __global__ void k_values(JobDev* jobs, PageDev* pages, const PartRec* parts, con
                          uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks);
 __global__ void k_dict_plan(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total,
                             uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks,
-                            VRec* recs);
+                            VRec* recs, int walk_small);
 __global__ void k_dict4(PageDev* pages, const int* total, int* queue, const VRec* recs);
+__global__ void k_dict_walk(PageDev* pages, const int* total, int* queue, const VRec* recs);
+__global__ void k_dict_walk_g(PageDev* pages, const int* total, int* queue, const VRec* recs);
 __global__ void k_finalize(JobDev* jobs, int n_jobs, PageDev* pages);
 __global__ void k_str_dict(JobDev* jobs, PageDev* pages, int64_t* doffs_arena);
 __global__ void k_str_count(JobDev* jobs, PageDev* pages, PartRec* parts, const int* total, int* queue,
@@ -170,8 +172,11 @@ struct pqg_ctx {
   int num_cus = 256;
   DevBuf vrecs;          // VRec per page-list entry (k_dict_plan -> k_dict4)
   int dict4_per_cu = 2;  // resident k_dict4 workgroups per CU (LDS-bound), from the occupancy query
+  int dict_walk_per_cu = 2;  // the same for k_dict_walk
+  int dict_walkg_per_cu = 2; // and k_dict_walk_g
   int dict4_threads = 256;
   bool dict4 = true;     // k_dict4 for 4-byte dictionary pages (PQG_DICT4=0: k_values<1>, for A/B runs)
+  bool dict_walk = true; // k_dict4 walks small pages' index streams itself (PQG_DICT_WALK=0: k_hybrid_walk run tables)
   int snappy_per_cu = 2;  // resident k_snappy waves per CU (LDS-bound: the output history ring)
   DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
   DevBuf tile_job;  // K1: tile -> job
@@ -256,6 +261,7 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
   for (auto& e : c->ev) hipEventCreate(&e);
   for (auto& e : c->ev_k8) hipEventCreate(&e);
   if (const char* e = getenv("PQG_DICT4")) c->dict4 = atoi(e) != 0;
+  if (const char* e = getenv("PQG_DICT_WALK")) c->dict_walk = atoi(e) != 0;
   {
     hipFuncAttributes fa;
     if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_dict4)) == hipSuccess && fa.maxThreadsPerBlock > 0)
@@ -264,6 +270,14 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, reinterpret_cast<const void*>(&k_dict4), c->dict4_threads, 0) ==
             hipSuccess && o > 0)
       c->dict4_per_cu = o;
+    o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, reinterpret_cast<const void*>(&k_dict_walk), c->dict4_threads, 0) ==
+            hipSuccess && o > 0)
+      c->dict_walk_per_cu = o;
+    o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, reinterpret_cast<const void*>(&k_dict_walk_g), c->dict4_threads, 0) ==
+            hipSuccess && o > 0)
+      c->dict_walkg_per_cu = o;
   }
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&k_snappy), 64, 0) ==
@@ -563,8 +577,9 @@ static int launch_pipeline(pqg_ctx* c) {
       1, std::min<int64_t>((c->list_cap + kWalkLanes - 1) / kWalkLanes, c->num_cus * (2048 / kWalkLanes)));
   LongWalk* wlong = (LongWalk*)c->walk_long.p;
   const int wlc = (int)std::min<int64_t>(c->walk_long_cap, INT32_MAX);
+  const int walk_small = c->dict4 && c->dict_walk;  // small 4-byte dictionary pages: walked in k_dict4
   hipLaunchKernelGGL(k_hybrid_walk, dim3(walk_blocks), dim3(kWalkLanes), 0, s, pages, list, ctr, streams, runs, blks,
-                     wlong, wlc);
+                     wlong, wlc, walk_small);
   hipLaunchKernelGGL(k_walk_long, dim3(c->num_cus * 2), dim3(256), 0, s, ctr, wlong, wlc, blks);
   if (c->timed) hipEventRecord(c->ev[5], s);
   if (c->timed) hipEventRecord(c->ev[6], s);
@@ -577,9 +592,16 @@ static int launch_pipeline(pqg_ctx* c) {
   if (c->dict4) {  // 4-byte dictionary pages: pieces staged in LDS, small dictionaries in LDS (pqg_dict.hip)
     VRec* recs = (VRec*)c->vrecs.p;
     hipLaunchKernelGGL(k_dict_plan, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((items_cap + 255) / 256, c->num_cus * 4))),
-                       dim3(256), 0, s, jobs, pages, parts, ctr, (uint8_t*)c->value_arena.p, streams, runs, blks, recs);
+                       dim3(256), 0, s, jobs, pages, parts, ctr, (uint8_t*)c->value_arena.p, streams, runs, blks, recs,
+                       walk_small);
     hipLaunchKernelGGL(k_dict4, dim3(qgrid(c->num_cus * c->dict4_per_cu)), dim3(c->dict4_threads), 0, s, pages, ctr, Q(3),
                        recs);
+    if (walk_small) {
+      hipLaunchKernelGGL(k_dict_walk, dim3(qgrid(c->num_cus * c->dict_walk_per_cu)), dim3(c->dict4_threads), 0, s, pages,
+                         ctr, Q(kQueueDictWalk), recs);
+      hipLaunchKernelGGL(k_dict_walk_g, dim3(qgrid(c->num_cus * c->dict_walkg_per_cu)), dim3(c->dict4_threads), 0, s,
+                         pages, ctr, Q(kQueueDictWalkG), recs);
+    }
   } else
     hipLaunchKernelGGL(k_values<1>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, parts, ctr, Q(3),
                        (uint8_t*)c->value_arena.p, streams, runs, blks);
@@ -805,14 +827,14 @@ int pqg_decode_page(pqg_ctx* c, const pqg_page_job* pj, pqg_chunk_result* result
 
 // gzipCompressor.DecompressBlock (compress.go:63-76): gzip.NewReader +
 // ioutil.ReadAll.  The decoded length is not in the block, so k_inflate decodes
-// it as a bare block (kPageBareBlock): bytes past `cap` are counted and CRC'd
-// but not stored, and the count comes back in PageDev.gz_len.
-static int block_inflate(pqg_ctx* c, const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int64_t* out_len) {
-  const int64_t store = std::min<int64_t>(std::max<int64_t>(cap, 0), INT32_MAX);
-  hipSetDevice(c->device);
-  if (c->blk_src.grow((size_t)n + 64) || c->blk_dst.grow((size_t)store + 64) ||
-      c->blk_meta.grow(sizeof(JobDev) + sizeof(PageDev) + (4 + 2 * kQueueInts) * sizeof(int)))
-    return PQG_ERR_HIP;
+// it as a bare block (kPageBareBlock): bytes past the device buffer's `store`
+// are counted and CRC'd but not stored, and the count comes back in
+// PageDev.gz_len.  The first pass stores at most kInflateFirst bytes; a block
+// that decodes to more (and fits `cap`) is decoded again into a buffer of its
+// size, so the device buffer never grows to `cap` before the length is known,
+// and no byte past what k_inflate stored is ever copied out.
+static int inflate_pass(pqg_ctx* c, int64_t n, int64_t store, PageDev* out) {
+  if (c->blk_dst.grow((size_t)store + 64)) return PQG_ERR_HIP;
   JobDev jd;
   memset(&jd, 0, sizeof(jd));
   jd.data = (const uint8_t*)c->blk_src.p;
@@ -832,8 +854,7 @@ static int block_inflate(pqg_ctx* c, const uint8_t* src, int64_t n, uint8_t* dst
   PageDev* dpage = (PageDev*)(meta + sizeof(JobDev));
   int* ints = (int*)(meta + sizeof(JobDev) + sizeof(PageDev));  // [0] list, [1] total, then the queue
   int hi[2] = {0, 1};
-  if ((n && hipMemcpyAsync(c->blk_src.p, src, (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess) ||
-      hipMemcpyAsync(djob, &jd, sizeof(jd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+  if (hipMemcpyAsync(djob, &jd, sizeof(jd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(dpage, &pd, sizeof(pd), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(ints, hi, sizeof(hi), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemsetAsync(ints + 4, 0, sizeof(int) * kQueueInts, c->stream) != hipSuccess)
@@ -841,12 +862,35 @@ static int block_inflate(pqg_ctx* c, const uint8_t* src, int64_t n, uint8_t* dst
   hipLaunchKernelGGL(k_inflate, dim3(qgrid(1)), dim3(64), 0, c->stream, djob, dpage, ints, ints + 1, ints + 4,
                      (uint8_t*)c->blk_dst.p);
   if (hipGetLastError() != hipSuccess) return PQG_ERR_HIP;
-  if (hipMemcpyAsync(&pd, dpage, sizeof(pd), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+  if (hipMemcpyAsync(out, dpage, sizeof(PageDev), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return PQG_ERR_HIP;
+  return PQG_OK;
+}
+
+static int block_inflate(pqg_ctx* c, const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap, int64_t* out_len) {
+  constexpr int64_t kInflateFirst = 64 << 20;
+  hipSetDevice(c->device);
+  if (c->blk_src.grow((size_t)n + 64) ||
+      c->blk_meta.grow(sizeof(JobDev) + sizeof(PageDev) + (4 + 2 * kQueueInts) * sizeof(int)))
+    return PQG_ERR_HIP;
+  if (n && hipMemcpyAsync(c->blk_src.p, src, (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    return PQG_ERR_HIP;
+  int64_t store = std::min<int64_t>(std::max<int64_t>(cap, 0), kInflateFirst);
+  PageDev pd;
+  int e = inflate_pass(c, n, store, &pd);
+  if (e) return e;
   if (pd.read_status != kOK) return pd.read_status;
   *out_len = pd.gz_len;
   if (pd.gz_len > cap) return PQG_ERR_CAPACITY;
+  if (pd.gz_len > INT32_MAX) return PQG_ERR_UNSUPPORTED;  // one block of >= 2 GiB: the kernel's 32-bit offsets
+  if (pd.gz_len > store) {  // decoded length known now: again, storing all of it
+    store = pd.gz_len;
+    e = inflate_pass(c, n, store, &pd);
+    if (e) return e;
+    if (pd.read_status != kOK) return pd.read_status;
+    if (pd.gz_len != store) return PQG_ERR_HIP;  // the same bytes decode to the same length
+  }
   if (pd.gz_len && (hipMemcpyAsync(dst, c->blk_dst.p, (size_t)pd.gz_len, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
                     hipStreamSynchronize(c->stream) != hipSuccess))
     return PQG_ERR_HIP;

@@ -651,7 +651,7 @@ __global__ void __launch_bounds__(64) k_str_count(JobDev* jobs, PageDev* pages, 
                                                   const RunEnt* runs, const BlockDesc* blks) {
   __shared__ __attribute__((aligned(16))) ExpandShared sh;
   const int lane = lane_id();
-  const int n_items = total[kCtrItems];
+  const int n_items = min(total[kCtrItems], total[kCtrPartsCap]);
   for (;;) {
     const int t = queue_next(queue);
     if (t >= n_items) return;
@@ -826,6 +826,61 @@ struct DbpWalk32 {
     position += 8;
     return kOK;
   }
+  // group() for every remaining position (position .. total), without the
+  // values: the reader ends where those calls would leave it, with their
+  // errors.  One step per run of groups inside one miniblock (a miniblock
+  // starts at a group start that is a multiple of mbvc), so the work is
+  // bounded by the stream's bytes (every miniblock has a width byte), not by
+  // the header's count (the oracle's DeltaBP::skip_rest).  Wave-uniform.
+  __device__ int skip_rest() {
+    const int64_t L = (int64_t)mbvc / gcd8(mbvc) * 8;  // lcm(8, mbvc)
+    const int64_t last = ((int64_t)total - 1) / 8 * 8;  // the group holding the last value
+    while (position < total) {
+      if (position % mbvc == 0) {
+        if (cur >= mbc) {
+          const int e = mini_header();
+          if (e) return e;
+        }
+        cw = win.get(wpos + cur);
+        mbpos = 0;
+        cur++;
+      }
+      const int64_t next_start = ((int64_t)position / L + 1) * L;
+      const bool tail = last < next_start;
+      const int64_t g = tail ? (last - position) / 8 + 1 : (next_start - position) / 8;
+      if (win.n - r < g * cw) {  // io.ReadFull of a group
+        r = win.n;
+        return kEOF;
+      }
+      r += g * cw;
+      mbpos = (int32_t)((uint32_t)mbpos + (uint32_t)(g * cw));
+      if (!tail) {
+        position = (int32_t)next_start;
+        continue;
+      }
+      const int64_t l = (int64_t)(mbvc / 8) * cw - mbpos;
+      if (l < 0) return kDELTA;  // "invalid stream"
+      r = r + l < win.n ? r + l : win.n;  // errors ignored
+      if (cur < mbc) {
+        const int w2 = win.get(wpos + cur);  // sic: miniBlockBitWidth[currentMiniBlock]
+        if (w2 != 0) {
+          const int64_t skip = (int64_t)(mbc - cur) * (int64_t)(mbvc / 8) * w2;
+          r = r + skip < win.n ? r + skip : win.n;
+        }
+      }
+      position = total;
+    }
+    return kOK;
+  }
+  __device__ static int64_t gcd8(int32_t v) {
+    int64_t a = v, b = 8;
+    while (b) {
+      const int64_t t = a % b;
+      a = b;
+      b = t;
+    }
+    return a;
+  }
 };
 
 // One wave per DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY page: the read phase
@@ -860,26 +915,29 @@ __global__ void __launch_bounds__(64) k_str_delta(JobDev* jobs, PageDev* pages, 
     const int64_t nn = pg.decode_status == kOK ? pg.not_null : 0;
     // ---- read phase: lengths (DBA: prefixes, then suffix lengths)
     DbpWalk32 A, B;  // A: prefix lengths (DBA) / lengths; B: suffix lengths (DBA)
-    // a length count beyond the page's NumValues is refused (the oracle's
-    // DeltaLength::init: unbounded work for zero-width miniblocks otherwise)
+    // every length of the header's count is read (type_bytearray.go:104-113,
+    // 195-207); those past the page's NumValues are never used, so they are
+    // walked by miniblock (skip_rest: work bounded by the stream's bytes)
     int re = A.init(val, vn, lds_ptr(sh.win[0]), 0);
-    if (re == kOK && A.total > pg.num_values) re = kDELTA;
     int64_t a_end = 0;
     if (re == kOK) {
-      for (int32_t p = 0; p < A.total && re == kOK; p += 8) {
+      const int32_t keep = A.total < pg.num_values ? A.total : pg.num_values;
+      for (int32_t p = 0; p < keep && re == kOK; p += 8) {
         int32_t v;
         re = A.group(&v);
       }
+      if (re == kOK) re = A.skip_rest();
       a_end = A.r;
     }
     if (re == kOK && dba) {
       re = B.init(val, vn, lds_ptr(sh.win[1]), a_end);
-      if (re == kOK && B.total > pg.num_values) re = kDELTA;
       if (re == kOK) {
-        for (int32_t p = 0; p < B.total && re == kOK; p += 8) {
+        const int32_t keep = B.total < pg.num_values ? B.total : pg.num_values;
+        for (int32_t p = 0; p < keep && re == kOK; p += 8) {
           int32_t v;
           re = B.group(&v);
         }
+        if (re == kOK) re = B.skip_rest();
       }
       if (re == kOK && A.total != B.total) re = kDELTA;  // "different number of suffixes and prefixes"
     }
@@ -1207,7 +1265,7 @@ __global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, 
   __shared__ int64_t part[9];
   __shared__ __attribute__((aligned(16))) uint8_t stage[kCopyStage];
   __shared__ __attribute__((aligned(16))) uint8_t sstage[kSrcStage + 16];  // PLAIN / DLBA sources of a round
-  const int n_items = total[kCtrItems];
+  const int n_items = min(total[kCtrItems], total[kCtrPartsCap]);
   for (;;) {
     if (threadIdx.x == 0) s_t = queue_pull(queue);
     __syncthreads();

@@ -807,7 +807,7 @@ __global__ void __launch_bounds__(64, Mode == 3 ? PQG_DBP_WPE : PQG_VALUES_WPE) 
   __shared__ __attribute__((aligned(16))) ValuesShared sh;
   const int lane = lane_id();
   if (total[kModePresentOff + Mode] == 0) return;  // no page of this stage
-  const int n_items = total[kCtrItems];
+  const int n_items = min(total[kCtrItems], total[kCtrPartsCap]);
   for (;;) {
     PQG_T(tp0);
     const int t = queue_next(queue);

@@ -82,6 +82,17 @@ def _dba(prefix, suffix_lens, chars):
     return W.dbp_encode(np.asarray(prefix, dtype=np.int32), bits=32) + _dlba(suffix_lens, chars)
 
 
+def _huge_dlba(length, count, bad_width=False):
+    """A DBP length stream announcing `count` lengths all equal to `length`:
+    blocks of 2^30 values, 4 zero-width miniblocks each (a second block's
+    widths > 32 with bad_width)."""
+    bs = 1 << 30
+    out = U.uvarint(bs) + U.uvarint(4) + U.uvarint(count) + U.zigzag(length)
+    for b in range(-(-(count - 1) // bs)):
+        out += U.uvarint(0) + bytes([40 if (bad_width and b == 1) else 0] * 4)
+    return out
+
+
 def _page_chunk(values_section, nvals, enc):
     return U.v1_page(values_section, nvals, enc)
 
@@ -103,8 +114,14 @@ def hand_cases():
          abi.STATUS_CODES["EOF"]),
         # Q3: one length, no miniblock header -> init fails (EOF)
         ("dlba_one_value", _page_chunk(_dlba([3], b"abc"), 1, DLBA), abi.STATUS_CODES["EOF"]),
-        # more lengths than the page's values: refused
-        ("dlba_count_guard", _page_chunk(_dlba(ok_lens, chars), 4, DLBA), abi.STATUS_CODES["DELTA"]),
+        # more lengths than the page's values: every length is decoded (type_bytearray.go:104-113),
+        # the value bytes start after all of them, the page takes its first 4 values
+        ("dlba_more_lens", _page_chunk(_dlba(ok_lens, chars), 4, DLBA), 0),
+        ("dba_more_lens", _page_chunk(_dba([0, 2, 2, 0, 1, 1, 0, 2, 2], ok_lens, chars), 5, DBA), 0),
+        # ~2^31 zero-width lengths announced by two block headers: walked by block, not by value
+        ("dlba_huge_count", _page_chunk(_huge_dlba(3, 2_000_000_000) + b"abcdefghi", 3, DLBA), 0),
+        ("dlba_huge_count_bad_tail", _page_chunk(_huge_dlba(3, 2_000_000_000, bad_width=True) + b"abcdefghi", 3,
+                                                 DLBA), abi.STATUS_CODES["BIT_WIDTH"]),
         ("dba_ok", _page_chunk(_dba([0, 2, 2, 0, 1, 1, 0, 2, 2], ok_lens, chars), n, DBA), 0),
         # prefix longer than the previous value -> "invalid prefix len in the stream"
         ("dba_prefix_too_long", _page_chunk(_dba([0, 2, 2, 0, 9, 1, 0, 2, 2], ok_lens, chars), n, DBA),
@@ -129,6 +146,10 @@ def test_oracle_hand_pages(case):
     assert r.status == want, "%s: %s" % (name, abi.status_name(r.status))
     if name == "dlba_ok":
         assert b"".join(_strings(r)) == bytes(range(97, 97 + 28))
+    if name == "dlba_more_lens":
+        assert _strings(r) == [b"abc", b"", b"defgh", b"ij"]
+    if name == "dlba_huge_count":
+        assert _strings(r) == [b"abc", b"def", b"ghi"]
     if name == "dba_ok":
         got = _strings(r)
         assert len(got) == 9 and got[1][:2] == got[0][:2]
@@ -276,3 +297,48 @@ def test_gpu_flba_hand_pages(dec, case):
 def test_gpu_flba_generated(dec):
     data, _ = _flba_file()
     P.compare_file(data, dec)
+
+
+def _odd_dbp(rng, n):
+    """A DBP stream of n int32 values in an odd layout (block sizes not
+    multiples of 128, miniblocks of 12 or 20 values, random widths)."""
+    bs, mbc = [(12, 1), (40, 2), (24, 2), (128, 4), (64, 8)][int(rng.integers(0, 5))]
+    mbvc = bs // mbc
+    out = U.uvarint(bs) + U.uvarint(mbc) + U.uvarint(n) + U.zigzag(int(rng.integers(-50, 50)))
+    vals = n - 1
+    while vals > 0:
+        widths = [int(rng.integers(0, 9)) for _ in range(mbc)]
+        out += U.zigzag(int(rng.integers(-5, 5))) + bytes(widths)
+        for w in widths:
+            out += bytes(rng.integers(0, 256, (mbvc // 8) * w, dtype=np.uint8))
+        vals -= bs
+    return out
+
+
+def test_oracle_dbp_skip_matches_next():
+    """DeltaBP::skip_rest (lengths past NumValues) leaves the reader where
+    next() for every value would, with the same status, on standard and odd
+    layouts, truncated and mutated streams."""
+    rng = np.random.default_rng(404)
+    streams = []
+    for _ in range(60):
+        n = int(rng.integers(1, 3000))
+        base = W.dbp_encode(rng.integers(0, 40, n).astype(np.int32), bits=32) if rng.random() < 0.5 \
+            else _odd_dbp(rng, n)
+        streams.append(base)
+        streams.append(base[:int(rng.integers(1, len(base)))])
+        b = bytearray(base)
+        b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+        streams.append(bytes(b))
+    checked = 0
+    for s in streams:
+        rc_full, end_full, cnt = O.delta_lengths_end(s, 1 << 40)
+        if cnt > 200000:
+            continue
+        for keep in (0, 1, 5, 8, 9, 13, 64, 130, cnt // 2, max(cnt - 1, 0)):
+            rc, end, _ = O.delta_lengths_end(s, keep)
+            assert rc == rc_full, (keep, cnt, rc, rc_full)
+            if rc == 0:  # (a failing stream fails the page: its reader position is not used)
+                assert end == end_full, (keep, cnt, end, end_full)
+            checked += 1
+    assert checked > 1000

@@ -137,6 +137,32 @@ def _gz_with_header_fields(raw):
         (len(raw) & 0xffffffff).to_bytes(4, "little")
 
 
+def _gz_named(raw, name_len, comment_len=0):
+    """A member whose FNAME (and FCOMMENT) hold name_len (comment_len) bytes before the NUL."""
+    body = zlib.compressobj(6, zlib.DEFLATED, -15)
+    deflate = body.compress(raw) + body.flush()
+    flg = 0x08 | (0x10 if comment_len else 0)
+    hdr = bytes([0x1f, 0x8b, 8, flg, 0, 0, 0, 0, 0, 3]) + b"n" * name_len + b"\0"
+    if comment_len:
+        hdr += b"c" * comment_len + b"\0"
+    return hdr + deflate + (zlib.crc32(raw) & 0xffffffff).to_bytes(4, "little") + \
+        (len(raw) & 0xffffffff).to_bytes(4, "little")
+
+
+# Go's compress/gzip readString reads FNAME / FCOMMENT into a [512]byte buffer:
+# 511 bytes + the NUL decode, 512 bytes before the NUL fail with ErrHeader
+NAME_CASES = [(511, 0, 0), (512, 0, "GZIP"), (0, 511, 0), (3, 512, "GZIP"), (2000, 0, "GZIP")]
+
+
+@pytest.mark.parametrize("name_len,comment_len,want", NAME_CASES)
+def test_oracle_gzip_name_bound(name_len, comment_len, want):
+    raw = b"hello parquet " * 50
+    rc, out = O.gzip_decode(_gz_named(raw, name_len, comment_len))
+    assert rc == (abi.STATUS_CODES[want] if want else 0)
+    if not want:
+        assert out == raw
+
+
 def _gpu_blocks():
     rng = np.random.default_rng(44)
     rep = np.repeat(rng.integers(0, 50, 40000), rng.integers(1, 30, 40000)).astype(np.int64).tobytes()
@@ -278,3 +304,13 @@ def test_gpu_gzip_page_errors(dec, how):
     page = U.page_header_v1(ulen, len(gz), 3000, abi.ENC_PLAIN) + bytes(gz)
     exp, _ = P.compare_chunk_bytes(page, dec, ptype=abi.INT64, codec=abi.CODEC_GZIP)
     assert exp.status != 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name_len,comment_len,want", NAME_CASES)
+def test_gpu_gzip_name_bound(dec, name_len, comment_len, want):
+    raw = b"hello parquet " * 50
+    rc, n, dst = _gpu_block(dec, _gz_named(raw, name_len, comment_len), len(raw) + 16)
+    assert rc == (abi.STATUS_CODES[want] if want else 0), abi.status_name(rc)
+    if not want:
+        assert dst[:n].tobytes() == raw

@@ -196,3 +196,40 @@ def test_bench_launches_ranks():
     assert out.returncode == 0, out.stderr[-2000:]
     line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["verified_bit_exact"]
+
+
+def test_bench_gpus8_launch_touches_no_gpu(monkeypatch):
+    """`bench.py --gpus 8` (no launcher env) hands over to 8 ranks before any
+    GPU work: up to launch_ranks no decoder context is created, the HIP
+    library is not asked for, and torch.cuda is not initialised."""
+    import sys
+    import bench
+    import pqgpu
+    from pqgpu import _lib
+    calls = []
+    monkeypatch.setattr(pqgpu, "GpuDecoder", lambda *a, **k: calls.append("GpuDecoder"))
+    monkeypatch.setattr(_lib, "lib", lambda: calls.append("lib"))
+    seen = {}
+
+    def fake_launch(n):
+        torch = sys.modules.get("torch")
+        seen.update(n=n, calls=list(calls), cuda_init=bool(torch is not None and torch.cuda.is_initialized()))
+        return 0
+
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setattr(bench, "launch_ranks", fake_launch)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 0
+    assert seen == {"n": 8, "calls": [], "cuda_init": False}
+
+
+def test_rank_plans_for_eight_gpus():
+    """The row groups each of 8 ranks decodes (bench.py: C2 one row group per
+    width, C5 8 of the 64): disjoint, complete, equal work per rank."""
+    c5 = [list(shard.row_groups_for_rank(64, r, 8)) for r in range(8)]
+    assert sorted(sum(c5, [])) == list(range(64)) and all(len(x) == 8 for x in c5)
+    c2 = [list(shard.row_groups_for_rank(8, r, 8)) for r in range(8)]
+    assert c2 == [[r] for r in range(8)]

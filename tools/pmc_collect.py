@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""profiles/<tag>_pmc_<config>.json from the PMC passes of tools/r04_pmc.sh:
-for each config, the workload description and the chunk bytes (the K1
-scan's algorithmic bytes, which FETCH_SIZE is calibrated on) come from the
-bench line the FETCH_SIZE pass printed; tools/pmc_traffic.py does the rest.
-Usage: pmc_collect.py <gpurun_out dir> <tag> [configs...]"""
+"""profiles/<tag>_pmc_<config>.json from the PMC passes of tools/gpu_steps.sh
+(steps pmc:<cfg>:FETCH_SIZE and pmc:<cfg>:WRITE_SIZE): for each config, the
+workload description and the chunk bytes (the K1 scan's algorithmic bytes,
+which FETCH_SIZE is calibrated on) come from the bench line the FETCH_SIZE
+pass printed; tools/pmc_traffic.py does the rest.
+Usage: pmc_collect.py <gpurun_out/TAG dir> <tag> [configs...]"""
 import json
 import os
 import sys
@@ -16,9 +17,9 @@ import pmc_traffic  # noqa: E402
 def main(out_dir, tag, configs):
     root = os.path.dirname(HERE)
     for cfg in configs:
-        line = os.path.join(out_dir, "pmc_fetch_%s.json" % cfg)
-        fetch = os.path.join(out_dir, "pmc", "fetch_%s_counter_collection.csv" % cfg)
-        write = os.path.join(out_dir, "pmc", "write_%s_counter_collection.csv" % cfg)
+        line = os.path.join(out_dir, "pmc_%s_FETCH_SIZE.out" % cfg)
+        fetch = os.path.join(out_dir, "pmc", "%s_FETCH_SIZE_counter_collection.csv" % cfg)
+        write = os.path.join(out_dir, "pmc", "%s_WRITE_SIZE_counter_collection.csv" % cfg)
         if not (os.path.exists(line) and os.path.exists(fetch) and os.path.exists(write)):
             print(cfg, "missing PMC outputs")
             continue

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-launch HBM traffic of each kernel from two rocprofv3 --pmc passes
-(FETCH_SIZE and WRITE_SIZE, separate runs: tools/gpu_pmc.sh) → JSON read by
+(FETCH_SIZE and WRITE_SIZE, separate runs: tools/gpu_steps.sh pmc steps) → JSON read by
 bench.py for roofline.traffic.  Both counters are in KiB.
 
 FETCH_SIZE is calibrated on this run's own known-byte kernel: k_page_cands
