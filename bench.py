@@ -114,6 +114,12 @@ def gen_workload(key, args, rank, world):
         desc = ("C3: INT64 timestamps, %d rows, DELTA_BINARY_PACKED (128/4x32), V2, SNAPPY, 20000 rows/page"
                 % args.c3_rows)
         dtype = "int64"
+    elif key == "c3_gzip":
+        data, info = W.config_c3(rows=args.c3gz_rows, codec=W.GZIP)
+        files.append((pqgpu.ParquetFile(data), [(0, 0)], ("flat", [info["values"]])))
+        desc = ("C3-GZIP: the C3 column (INT64 timestamps, DELTA_BINARY_PACKED, V2, 20000 rows/page), %d rows, "
+                "GZIP pages (one zlib-default member per page, as Go's gzip.NewWriter)" % args.c3gz_rows)
+        dtype = "int64"
     elif key == "c4":
         data, info = W.config_c4(rows=args.c4_rows)
         files.append((pqgpu.ParquetFile(data), [(0, 0)], ("str", info)))
@@ -150,7 +156,10 @@ def _level_sections(pf, meta, pg, desc):
         return 0, pg.uncompressed_size
     at = meta.start + pg.payload_offset
     body = pf.data[at:at + pg.compressed_size]
-    if meta.codec != 0:
+    if meta.codec == 2:
+        import gzip
+        body = gzip.decompress(body)
+    elif meta.codec != 0:
         import pyarrow as pa
         body = pa.decompress(body, decompressed_size=pg.uncompressed_size, codec="snappy").to_pybytes()
     pos = 0
@@ -294,7 +303,8 @@ def cpu_baseline(wl, seconds):
 
 # ---------------------------------------------------------------- PMC traffic (committed passes)
 STAGE_KERNELS = {"scan": ["k_tile_jobs", "k_page_cands", "k_cand_parse", "k_tile_scan", "k_cand_link", "k_page_chain",
-                          "k_scan_pages"], "list": ["k_page_list"], "snappy": ["k_snap_plan", "k_snap_seg", "k_snap_link", "k_snap_decode", "k_snappy"], "levels": ["k_page_levels"],
+                          "k_scan_pages"], "list": ["k_page_list"], "snappy": ["k_snap_plan", "k_snap_seg", "k_snap_link", "k_snap_decode", "k_snappy",
+                                                     "k_inflate"], "levels": ["k_page_levels"],
                  "walk": ["k_hybrid_walk"], "unused": [], "nn_scan": ["k_nn_scan"],
                  "values": ["k_values", "k_dict_plan", "k_dict4", "k_dict_walk"], "strings": ["k_str_dict", "k_str_plain", "k_str_count", "k_char_scan",
                                                   "k_str_copy"],
@@ -342,15 +352,22 @@ def run_workload(wl, dec, args, steps, warmup, barrier, dist, world, rank, cpu_s
         step()
     bad = [abi.status_name(res[i].status) for i in range(n) if res[i].status != 0]
     assert not bad, "%s: %s" % (wl.key, bad)
-    stage_acc = np.zeros(len(STAGES))
+    # the timed steps run without the per-stage HIP events (instrumentation,
+    # a few us of stream time each); the stage breakdown comes from as many
+    # instrumented steps after them
+    L.pqg_set_timing(dec.ctx, 0)
     barrier()
     t_start = time.perf_counter()
     for _ in range(steps):
         step()
-        k = L.pqg_last_timings(dec.ctx, tmp, 16)
-        stage_acc += np.array([tmp[i] for i in range(1, min(k, 1 + len(STAGES)))])
     t_end = time.perf_counter()
     barrier()
+    L.pqg_set_timing(dec.ctx, 1)
+    stage_acc = np.zeros(len(STAGES))
+    for _ in range(steps):
+        step()
+        k = L.pqg_last_timings(dec.ctx, tmp, 16)
+        stage_acc += np.array([tmp[i] for i in range(1, min(k, 1 + len(STAGES)))])
     elapsed = t_end - t_start
     if dist is not None:
         import torch
@@ -500,11 +517,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=100_000_000, help="C2 rows per file")
     ap.add_argument("--bits", type=str, default="1,2,4,8,12,16,20")
-    ap.add_argument("--configs", type=str, default="c1,c1_1page,c2_run_heavy,c3,c4,c5",
+    ap.add_argument("--configs", type=str, default="c1,c1_1page,c2_run_heavy,c3,c3_gzip,c4,c5",
                     help="sub-results besides the C2 headline")
     ap.add_argument("--sub-steps", type=int, default=5)
     ap.add_argument("--c1-rows", type=int, default=10_000_000)
     ap.add_argument("--c3-rows", type=int, default=200_000_000)
+    ap.add_argument("--c3gz-rows", type=int, default=50_000_000)
     ap.add_argument("--c4-rows", type=int, default=50_000_000)
     ap.add_argument("--c5-rows-per-rg", type=int, default=15_625_000)
     ap.add_argument("--no-verify", action="store_true")

@@ -13,6 +13,7 @@
 #include <type_traits>
 #include <unordered_map>
 #include <vector>
+#include <zlib.h>
 
 namespace {
 
@@ -378,8 +379,25 @@ void write_page_header(Buf& out, int type, int32_t usize, int32_t csize, int32_t
   t.stop();
 }
 
+// GZIP (codec 2): one gzip member at zlib's default level, as Go's
+// gzip.NewWriter (compress.go:63-76 writes through compress/gzip's default).
+Buf gzip_compress(const uint8_t* src, int64_t n) {
+  z_stream z{};
+  if (deflateInit2(&z, Z_DEFAULT_COMPRESSION, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) return Buf();
+  Buf out(deflateBound(&z, (uLong)n) + 64);
+  z.next_in = const_cast<uint8_t*>(src);
+  z.avail_in = (uInt)n;
+  z.next_out = out.data();
+  z.avail_out = (uInt)out.size();
+  const int r = deflate(&z, Z_FINISH);
+  out.resize(r == Z_STREAM_END ? z.total_out : 0);
+  deflateEnd(&z);
+  return out;
+}
+
 Buf compress(int codec, const Buf& raw) {
   if (codec == 1) return snappy_compress(raw.data(), (int64_t)raw.size());
+  if (codec == 2) return gzip_compress(raw.data(), (int64_t)raw.size());
   return raw;
 }
 

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FLBA = range(8)
 PLAIN, RLE_DICTIONARY, DELTA_BINARY_PACKED = 0, 8, 5
 DELTA_LENGTH_BYTE_ARRAY, DELTA_BYTE_ARRAY = 6, 7
-UNCOMPRESSED, SNAPPY = 0, 1
+UNCOMPRESSED, SNAPPY, GZIP = 0, 1, 2
 REQUIRED, OPTIONAL, LIST = 0, 1, 2
 REF_HYBRID = -1  # Column(hybrid_groups=...): parquet-go's writer layout (one bit-packed run per stream)
 

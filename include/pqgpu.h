@@ -272,6 +272,12 @@ int pqg_get_pages(pqg_ctx* ctx, int job, pqg_page_info* out, int cap);
  * number of entries written. */
 int pqg_last_timings(pqg_ctx* ctx, float* out, int cap);
 
+/* Per-stage HIP events on the ctx stream (on by default): `on` = 0 records
+ * none (pqg_last_timings then reports nothing new), 1 records them.  The
+ * events are instrumentation: each costs a few microseconds of stream time,
+ * which matters for small batches. */
+int pqg_set_timing(pqg_ctx* ctx, int on);
+
 /* Optional: run `iters` back-to-back decodes of the same jobs on the ctx
  * stream and return the device time in ms (used by bench.py).  */
 int pqg_bench_decode(pqg_ctx* ctx, const pqg_chunk_job* jobs, int n_jobs, int iters,

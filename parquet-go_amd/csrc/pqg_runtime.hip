@@ -57,6 +57,10 @@ __global__ void k_snap_decode(const JobDev* jobs, PageDev* pages, const SnapSub*
 __global__ void k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                               uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena,
                               LongLev* longs, int long_cap, LevPiece* pieces, int piece_cap);
+__global__ void k_dict_resolve(JobDev* jobs, int n_jobs, PageDev* pages, uint8_t* scratch);
+__global__ void k_page_fused(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                             uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena, LongLev* longs,
+                             int long_cap, LevPiece* pieces, int piece_cap, uint8_t* value_arena, uint64_t* lb);
 __global__ void k_level_long(PageDev* pages, const int* ctr, const LongLev* longs, int long_cap,
                              const LevPiece* pieces, int piece_cap, int* queue);
 __global__ void k_hybrid_walk(const PageDev* pages, const int* list, const int* total, HStream* streams,
@@ -174,9 +178,14 @@ struct pqg_ctx {
   int dict4_per_cu = 2;  // resident k_dict4 workgroups per CU (LDS-bound), from the occupancy query
   int dict_walk_per_cu = 2;  // the same for k_dict_walk
   int dict_walkg_per_cu = 2; // and k_dict_walk_g
+  int fused_per_cu = 12;     // resident k_page_fused waves per CU (one-wave blocks), from the occupancy query
   int dict4_threads = 256;
   bool dict4 = true;     // k_dict4 for 4-byte dictionary pages (PQG_DICT4=0: k_values<1>, for A/B runs)
-  bool dict_walk = true; // k_dict4 walks small pages' index streams itself (PQG_DICT_WALK=0: k_hybrid_walk run tables)
+  // Measured alternatives, off by default (C2 on one MI355X, r05_s8: run tables
+  // 3.15 ms/step, in-kernel walk 3.33, fused 3.86):
+  bool dict_walk = false; // PQG_DICT_WALK=1: k_dict_walk / k_dict_walk_g walk small pages' index streams themselves
+  bool fused = false;     // PQG_FUSED=1: k_page_fused, levels + small 4-byte dictionary pages in one pass
+  DevBuf lookback;       // k_page_fused: one look-back word per page
   int snappy_per_cu = 2;  // resident k_snappy waves per CU (LDS-bound: the output history ring)
   DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
   DevBuf tile_job;  // K1: tile -> job
@@ -262,6 +271,7 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
   for (auto& e : c->ev_k8) hipEventCreate(&e);
   if (const char* e = getenv("PQG_DICT4")) c->dict4 = atoi(e) != 0;
   if (const char* e = getenv("PQG_DICT_WALK")) c->dict_walk = atoi(e) != 0;
+  if (const char* e = getenv("PQG_FUSED")) c->fused = atoi(e) != 0;
   {
     hipFuncAttributes fa;
     if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_dict4)) == hipSuccess && fa.maxThreadsPerBlock > 0)
@@ -278,6 +288,10 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, reinterpret_cast<const void*>(&k_dict_walk_g), c->dict4_threads, 0) ==
             hipSuccess && o > 0)
       c->dict_walkg_per_cu = o;
+    o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, reinterpret_cast<const void*>(&k_page_fused), 64, 0) ==
+            hipSuccess && o > 0)
+      c->fused_per_cu = o;
   }
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&k_snappy), 64, 0) ==
@@ -304,7 +318,7 @@ void pqg_ctx_destroy(pqg_ctx* c) {
                     &c->ok2slot, &c->order, &c->asm_seg, &c->offs_arena, &c->doffs_arena, &c->page_stage,
                     &c->blk_src, &c->blk_dst, &c->blk_meta, &c->tile_job, &c->sn_subs, &c->sn_segpage, &c->sn_F,
                     &c->blk_subs, &c->blk_segpage, &c->blk_F, &c->vrecs, &c->parts, &c->lev_long, &c->lev_pieces,
-                    &c->walk_long})
+                    &c->walk_long, &c->lookback})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
   hipStreamDestroy(c->stream);
@@ -464,6 +478,7 @@ static int plan_batch(pqg_ctx* c) {
       c->runs.grow(sizeof(RunEnt) * (size_t)run_total + 8192) || c->blks.grow(sizeof(BlockDesc) * (size_t)blk_total + 8192) ||
       c->vrecs.grow(sizeof(VRec) * (size_t)std::max<int64_t>(c->parts_cap, 1)) ||
       c->offs_arena.grow(sizeof(int64_t) * (size_t)offs_total + 64) ||
+      c->lookback.grow(sizeof(uint64_t) * (size_t)std::max<int64_t>(page_total, 1)) ||
       c->doffs_arena.grow(sizeof(int64_t) * (size_t)doffs_total + 64))
     return PQG_ERR_HIP;
   c->total_tiles = tile_total;
@@ -568,8 +583,18 @@ static int launch_pipeline(pqg_ctx* c) {
   LongLev* llong = (LongLev*)c->lev_long.p;
   LevPiece* lpieces = (LevPiece*)c->lev_pieces.p;
   const int llc = (int)std::min<int64_t>(c->lev_long_cap, INT32_MAX), lpc = (int)std::min<int64_t>(c->lev_piece_cap, INT32_MAX);
-  hipLaunchKernelGGL(k_page_levels, dim3(qgrid(c->num_cus * 24)), dim3(64), 0, s, jobs, pages, list, ctr, Q(1), scratch,
-                     streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p, llong, llc, lpieces, lpc);
+  // each job's dictionary page (the fused kernel gathers from it)
+  hipLaunchKernelGGL(k_dict_resolve, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, jobs, n, pages, scratch);
+  const bool fused = c->fused && c->dict4 && c->dict_walk;
+  if (fused) {  // levels + the small 4-byte dictionary pages' values (pqg_fused.hip)
+    hipMemsetAsync(c->lookback.p, 0, sizeof(uint64_t) * (size_t)std::max<int64_t>(c->list_cap, 1), s);
+    hipLaunchKernelGGL(k_page_fused, dim3((unsigned)(c->num_cus * c->fused_per_cu)), dim3(64), 0, s, jobs, pages, list,
+                       ctr, Q(1), scratch, streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p, llong, llc,
+                       lpieces, lpc, (uint8_t*)c->value_arena.p, (uint64_t*)c->lookback.p);
+  } else {
+    hipLaunchKernelGGL(k_page_levels, dim3(qgrid(c->num_cus * 24)), dim3(64), 0, s, jobs, pages, list, ctr, Q(1), scratch,
+                       streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p, llong, llc, lpieces, lpc);
+  }
   hipLaunchKernelGGL(k_level_long, dim3(qgrid(c->num_cus * 8)), dim3(64), 0, s, pages, ctr, llong, llc, lpieces, lpc,
                      Q(kQueueLevLong));
   if (c->timed) hipEventRecord(c->ev[4], s);
@@ -1054,6 +1079,12 @@ int pqg_debug_job(pqg_ctx* c, int job, int64_t* out, int cap) {
   int k = 0;
   for (; k < 5 && k < cap; k++) out[k] = v[k];
   return k;
+}
+
+int pqg_set_timing(pqg_ctx* c, int on) {
+  if (!c) return PQG_ERR_INVALID_ARG;
+  c->timed = on != 0;
+  return PQG_OK;
 }
 
 int pqg_last_timings(pqg_ctx* c, float* out, int cap) {

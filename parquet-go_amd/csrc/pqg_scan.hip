@@ -155,35 +155,23 @@ __device__ __forceinline__ void init_job_results(JobDev& job) {
 }
 
 // ---- K1a ------------------------------------------------------------------
-// Byte source of the per-lane candidate parse.  Reads stop at `limit`
-// (kCandParseBytes past the candidate): a header that needs more is left to
-// the serial walk (`hit`), so a garbage candidate cannot run away through the
-// chunk (e.g. a thrift list header claiming 2^31 elements).
+// Byte source of the per-lane candidate parse: the candidate's first bytes,
+// prefetched into the lane's LDS window.  Reads stop at `limit` (the window's
+// end, at most kCandParseBytes past the candidate): a header that needs more
+// is left to the serial walk (`hit`), so a garbage candidate cannot run away
+// through the chunk (e.g. a thrift list header claiming 2^31 elements).
+// Bytes past the chunk read as -1 (EOF) without `hit`.
 constexpr int64_t kCandParseBytes = 1024;
-struct GlobalSrc {
-  gcu8 p;
-  int64_t n, limit;
+struct CandSrc {
+  const PQG_L uint8_t* win;  // bytes [wlo, limit) of the chunk
+  int64_t wlo, limit, n;
   bool hit;
-  uintptr_t gaddr;  // 16-byte granule held in `g` (0: none)
-  uint4 g;
-  const PQG_L uint8_t* win = nullptr;  // prefetched bytes [wlo, whi) (LDS), if any
-  int64_t wlo = 0, whi = 0;
   __device__ __forceinline__ int get(int64_t i) {
-    if (i >= limit && i < n) {
-      hit = true;
+    if (i >= limit) {
+      hit |= i < n;
       return -1;
     }
-    if (i < 0 || i >= n) return -1;
-    if (i >= wlo && i < whi) return win[i - wlo];
-    const uintptr_t a = (uintptr_t)(p + i);
-    const uintptr_t ga = a & ~(uintptr_t)15;
-    if (ga != gaddr) {  // the granule holds byte i < n: mapped
-      g = ldg16(ga);
-      gaddr = ga;
-    }
-    const int w = (int)((a >> 2) & 3);
-    const uint32_t d = w == 0 ? g.x : w == 1 ? g.y : w == 2 ? g.z : g.w;
-    return (int)((d >> (8 * (a & 3))) & 0xff);
+    return win[i - wlo];  // i >= wlo: the parse never reads before its candidate
   }
 };
 
@@ -193,6 +181,13 @@ __device__ __forceinline__ bool has_byte_15(uint32_t x) {
 }
 
 constexpr int kCandFrames = 4, kCandLast = 8;
+// Loop steps of one candidate parse (fields + skipped container elements):
+// the headers of parquet writers take at most ~25 (PageHeader, its page
+// header struct and a Statistics struct); garbage that runs longer is
+// kCOMPLEX (the serial walk reads it if a page link ever lands on it).  A
+// lane's steps set its wave's time: without the bound one garbage candidate
+// of ~80 one-byte fields held its wave ~0.2 ms.
+constexpr int kCandSteps = 40;
 
 // One lane parses and classifies the candidate at position p (kept out of
 // line: the scan loop around it must stay small).
@@ -205,8 +200,7 @@ constexpr int kCandFrames = 4, kCandLast = 8;
 constexpr int kCandWin = 10;  // granules: >= 144 bytes from any start
 __device__ __forceinline__ void parse_candidate(const JobDev& job, int64_t p, SkipFrame* frames, int16_t* lasts,
                                              PQG_L uint8_t* win, Cand* out) {
-  Compact<GlobalSrc> c;
-  c.src = GlobalSrc{gconst(job.data), job.data_len, p + kCandParseBytes, false, 0, make_uint4(0, 0, 0, 0)};
+  Compact<CandSrc> c;
   {
     const uintptr_t a0 = (uintptr_t)(job.data + p) & ~(uintptr_t)15;
     const int64_t lo = p - (int64_t)((uintptr_t)(job.data + p) - a0);  // chunk offset of the first granule
@@ -218,10 +212,9 @@ __device__ __forceinline__ void parse_candidate(const JobDev& job, int64_t p, Sk
     for (int k = 0; k < kCandWin; k++) g[k] = ldg16(lo + 16 * k < job.data_len ? a0 + 16 * k : a0);
 #pragma unroll
     for (int k = 0; k < kCandWin; k++) sts16(win + 16 * k, lo + 16 * k < job.data_len ? g[k] : make_uint4(0, 0, 0, 0));
-    c.src.win = win;
-    c.src.wlo = lo;
-    c.src.whi = lo + 16 * kCandWin < job.data_len ? lo + 16 * kCandWin : job.data_len;
-    if (c.src.whi < c.src.limit) c.src.limit = c.src.whi;
+    const int64_t whi = lo + 16 * kCandWin < job.data_len ? lo + 16 * kCandWin : job.data_len;
+    const int64_t lim = p + kCandParseBytes < whi ? p + kCandParseBytes : whi;
+    c.src = CandSrc{win, lo, lim, job.data_len, false};
   }
   // Structural pre-check: every thrift writer of PageHeader emits fields 1, 2,
   // 3 in id order with short-form i32 headers (15 t 15 <varint> 15).  A
@@ -252,6 +245,7 @@ __device__ __forceinline__ void parse_candidate(const JobDev& job, int64_t p, Sk
   c.bool_set = c.bool_val = false;
   c.fcap = kCandFrames;
   c.lcap = kCandLast;
+  c.budget = kCandSteps;
   PageHdr h;
   int e = c.read_page_header(&h);
   PageDev pg;

@@ -27,6 +27,13 @@
 
 namespace pqg {
 
+// the end-of-bytes shortcut of skip() (diagnostic builds may turn it off)
+#ifdef PQG_NO_EOF_SKIP
+constexpr bool kEofSkip = false;
+#else
+constexpr bool kEofSkip = true;
+#endif
+
 enum : int { T_STOP = 0, T_BOOL = 2, T_BYTE = 3, T_DOUBLE = 4, T_I16 = 6, T_I32 = 8, T_I64 = 10,
              T_STRING = 11, T_STRUCT = 12, T_MAP = 13, T_SET = 14, T_LIST = 15 };
 
@@ -58,6 +65,10 @@ struct Compact {
   int fcap = kMaxFrames;
   int lcap = kMaxLast;
   bool overflow = false;
+  // Loop steps left (fields read plus container elements skipped): the
+  // speculative candidate parse bounds its work with it (running out is
+  // `overflow`, like the small stacks); the serial walk never runs out.
+  int budget = 0x7fffffff;
 
   PQG_TINLINE int byte(uint8_t* b) {
     int v = src.get(pos);
@@ -241,193 +252,211 @@ struct Compact {
     }
     return -1;  // STOP / unknown: "Unknown data type"
   }
-  // protocol.go Skip(fieldType, depth) — iterative.
+  // protocol.go Skip(fieldType, depth) — iterative: start_value, then
+  // skip_step until the value's frames are all closed.
   PQG_TINLINE int skip(int type, int depth) {
     int nf = 0;
     int e = start_value(type, depth, &nf);
     for (;;) {
-      if (e) {  // unwind to the nearest MAP frame whose value is in flight
-        while (nf > 0 && !(frames[nf - 1].kind == T_MAP && frames[nf - 1].phase == 2)) nf--;
-        if (nf == 0) return -1;
-        e = 0;
+      const int r = skip_step(nf, e);
+      if (r <= 0) return r;
+    }
+  }
+  // One step of Skip: 1 = more to do, 0 = the value is skipped, -1 = error.
+  // `e`: the error of the previous step's start_value (unwinds to the nearest
+  // MAP frame whose value is in flight: that error is ignored).
+  PQG_TINLINE int skip_step(int& nf, int& e) {
+    if (--budget < 0) {
+      overflow = true;
+      return -1;
+    }
+    if (e) {
+      while (nf > 0 && !(frames[nf - 1].kind == T_MAP && frames[nf - 1].phase == 2)) nf--;
+      if (nf == 0) return -1;
+      e = 0;
+    }
+    if (nf == 0) return 0;
+    SkipFrame& f = frames[nf - 1];
+    if (f.kind == T_STRUCT) {
+      int t, id;
+      field_begin(&t, &id);  // error => STOP
+      if (t == T_STOP) {
+        struct_end();
+        nf--;
+        return 1;
       }
-      if (nf == 0) return 0;
-      SkipFrame& f = frames[nf - 1];
-      if (f.kind == T_STRUCT) {
-        int t, id;
-        field_begin(&t, &id);  // error => STOP
-        if (t == T_STOP) {
-          struct_end();
-          nf--;
-          continue;
-        }
-        e = start_value(t, f.depth - 1, &nf);
-      } else if (f.kind == T_LIST) {
+      e = start_value(t, f.depth - 1, &nf);
+    } else if (f.kind == T_LIST) {
+      if (f.remaining <= 0) {
+        nf--;
+        return 1;
+      }
+      // At the end of the bytes a STRUCT element is a no-op (its
+      // ReadFieldBegin fails, the error is ignored: STOP), and so is every
+      // element after it: the rest of the list is skipped in one step
+      // instead of up to 2^31 (a garbage header with a huge list size would
+      // otherwise spin one lane for seconds).  Only where the element would
+      // have pushed its frame and lastField entry without hitting a limit.
+      if (kEofSkip && f.et == T_STRUCT && f.depth > 1 && nf < fcap && nlast < lcap && src.get(pos) < 0) {
+        nf--;
+        return 1;
+      }
+      f.remaining--;
+      e = start_value(f.et, f.depth - 1, &nf);
+    } else {  // MAP
+      if (f.phase == 2) f.phase = 0;
+      if (f.phase == 0) {
         if (f.remaining <= 0) {
           nf--;
-          continue;
+          return 1;
+        }
+        // the same for STRUCT keys at the end of the bytes when the value is
+        // not a container (its error is ignored, it leaves no state)
+        if (kEofSkip && f.kt == T_STRUCT && f.vt != T_STRUCT && f.vt != T_MAP && f.vt != T_SET && f.vt != T_LIST &&
+            f.depth > 1 && nf < fcap && nlast < lcap && src.get(pos) < 0) {
+          nf--;
+          return 1;
         }
         f.remaining--;
-        e = start_value(f.et, f.depth - 1, &nf);
-      } else {  // MAP
-        if (f.phase == 2) f.phase = 0;
-        if (f.phase == 0) {
-          if (f.remaining <= 0) {
-            nf--;
-            continue;
-          }
-          f.remaining--;
-          f.phase = 1;
-          e = start_value(f.kt, f.depth - 1, &nf);
-        } else {
-          f.phase = 2;
-          e = start_value(f.vt, 64, &nf);  // self.Skip(valueType): fresh depth, error ignored
-          if (e) e = 0;                    // a direct primitive error is swallowed here
-        }
-      }
-    }
-  }
-  // Statistics.Read: binary 1,2,5,6; i64 3,4.
-  PQG_TINLINE int read_statistics() {
-    if (struct_begin()) return -1;
-    for (;;) {
-      int t, id;
-      if (field_begin(&t, &id)) return -1;
-      if (t == T_STOP) break;
-      int e;
-      if ((id == 1 || id == 2 || id == 5 || id == 6) && t == T_STRING) {
-        e = binary_skip();
-      } else if ((id == 3 || id == 4) && t == T_I64) {
-        int64_t v;
-        e = i64(&v);
+        f.phase = 1;
+        e = start_value(f.kt, f.depth - 1, &nf);
       } else {
-        e = skip(t, 64);
+        f.phase = 2;
+        e = start_value(f.vt, 64, &nf);  // self.Skip(valueType): fresh depth, error ignored
+        if (e) e = 0;                    // a direct primitive error is swallowed here
       }
-      if (e) return -1;
     }
-    struct_end();
-    return 0;
+    return 1;
   }
+  // PageHeader.Read (parquet.go:5885-6008) with the nested readers it calls —
+  // DataPageHeader.Read :3993-4090, IndexPageHeader (no fields),
+  // DictionaryPageHeader.Read :4333-4400, DataPageHeaderV2.Read :4585-4722 and
+  // Statistics.Read — as ONE loop over a stack of known structs.  Every
+  // field of every known struct goes through the same field_begin / read /
+  // skip code, so the generic skip() is inlined once (nested readers with a
+  // skip() each made k_cand_parse ~100K instructions: the instruction cache,
+  // not the bytes, set its speed).  Per known struct: a field of the
+  // expected id and type is read (i32 kept, bool / i64 / binary read and
+  // dropped), any other field is skipped; ReadFieldBegin errors, read errors
+  // and skip errors fail the header; at STOP the struct's required fields
+  // must have been seen ("Required field ... is not set").
+  enum : int { S_PH = 0, S_DPH = 1, S_IDX = 2, S_DICT = 3, S_V2 = 4, S_STAT = 5 };
+  enum : int { A_SKIP = 0, A_I32 = 1, A_BOOL = 2, A_I64 = 3, A_BIN = 4, A_STRUCT = 5 };
   PQG_TINLINE int read_page_header(PageHdr* h) {
     int64_t start = pos;
     h->type = h->usize = h->csize = 0;
     h->num_values = h->encoding = h->def_enc = h->rep_enc = 0;
     h->v2_def_len = h->v2_rep_len = 0;
     h->has_dph = h->has_dict = h->has_v2 = 0;
-    bool st = false, su = false, sc = false;
+    // known-struct stack (PageHeader -> DPH / V2 -> Statistics: depth <= 3),
+    // held as packed scalars (no dynamically indexed local arrays)
+    uint32_t schs = S_PH;  // 4 bits per level
+    uint32_t seen = 0;     // required fields of the innermost struct
+    uint32_t seen_up = 0;  // 8 bits per enclosing level
+    int depth = 1;
+    // a field being skipped: its frames and pending error (skip_step)
+    int nf = 0, se = 0;
+    bool skipping = false;
     if (struct_begin()) return kTHRIFT;
+    // ONE loop for both kinds of step: lanes of a wave parsing different
+    // candidates then step together (nested loops would run one lane's skip
+    // while the others wait, and the next lane's after it)
     for (;;) {
-      int t, id;
-      if (field_begin(&t, &id)) return kTHRIFT;
-      if (t == T_STOP) break;
-      int e = 0;
-      bool handled = false;
-      switch (id) {
-        case 1: if (t == T_I32) { handled = true; st = true; e = i32(&h->type); } break;
-        case 2: if (t == T_I32) { handled = true; su = true; e = i32(&h->usize); } break;
-        case 3: if (t == T_I32) { handled = true; sc = true; e = i32(&h->csize); } break;
-        case 4: if (t == T_I32) { handled = true; int32_t crc; e = i32(&crc); } break;
-        case 5:
-          if (t == T_STRUCT) {
-            handled = true;
-            h->has_dph = 1;
-            e = read_dph(h);
-          }
-          break;
-        case 6:
-          if (t == T_STRUCT) {  // IndexPageHeader has no fields: every field is skipped
-            handled = true;
-            if (struct_begin()) return kTHRIFT;
-            for (;;) {
-              int t2, id2;
-              if (field_begin(&t2, &id2)) return kTHRIFT;
-              if (t2 == T_STOP) break;
-              if (skip(t2, 64)) return kTHRIFT;
-            }
-            struct_end();
-          }
-          break;
-        case 7:
-          if (t == T_STRUCT) {
-            handled = true;
-            h->has_dict = 1;
-            e = read_dict(h);
-          }
-          break;
-        case 8:
-          if (t == T_STRUCT) {
-            handled = true;
-            h->has_v2 = 1;
-            e = read_v2(h);
-          }
-          break;
+      if (skipping) {
+        const int r = skip_step(nf, se);
+        if (r < 0) return kTHRIFT;
+        skipping = r > 0;
+        continue;
       }
-      if (!handled) e = skip(t, 64);
+      int t, id;
+      if (--budget < 0) {
+        overflow = true;
+        return kTHRIFT;
+      }
+      if (field_begin(&t, &id)) return kTHRIFT;
+      const int sc = (int)((schs >> (4 * (depth - 1))) & 0xf);
+      if (t == T_STOP) {
+        struct_end();
+        const uint32_t need = sc == S_PH ? 7u : sc == S_DPH ? 15u : sc == S_DICT ? 3u : sc == S_V2 ? 63u : 0u;
+        if ((seen & need) != need) return kTHRIFT;
+        if (--depth == 0) break;
+        seen = seen_up & 0xff;
+        seen_up >>= 8;
+        continue;
+      }
+      // the field's action in its struct: A_I32 into slot `slot` (required
+      // bit `bit`), A_STRUCT into schema `child`, or a read / skip
+      int act = A_SKIP, slot = -1, child = 0;
+      uint32_t bit = 0;
+      if (sc == S_PH) {
+        if (id >= 1 && id <= 4 && t == T_I32) { act = A_I32; slot = id - 1; bit = id <= 3 ? 1u << (id - 1) : 0u; }
+        else if (id == 5 && t == T_STRUCT) { act = A_STRUCT; child = S_DPH; }
+        else if (id == 6 && t == T_STRUCT) { act = A_STRUCT; child = S_IDX; }
+        else if (id == 7 && t == T_STRUCT) { act = A_STRUCT; child = S_DICT; }
+        else if (id == 8 && t == T_STRUCT) { act = A_STRUCT; child = S_V2; }
+      } else if (sc == S_DPH) {
+        if (id >= 1 && id <= 4 && t == T_I32) { act = A_I32; slot = 3 + id; bit = 1u << (id - 1); }
+        else if (id == 5 && t == T_STRUCT) { act = A_STRUCT; child = S_STAT; }
+      } else if (sc == S_DICT) {
+        if (id >= 1 && id <= 2 && t == T_I32) { act = A_I32; slot = 3 + id; bit = 1u << (id - 1); }
+        else if (id == 3 && t == T_BOOL) act = A_BOOL;
+      } else if (sc == S_V2) {
+        if (id >= 1 && id <= 6 && t == T_I32) { act = A_I32; slot = 8 + id; bit = 1u << (id - 1); }
+        else if (id == 7 && t == T_BOOL) act = A_BOOL;  // IsCompressed: ignored (Q4)
+        else if (id == 8 && t == T_STRUCT) { act = A_STRUCT; child = S_STAT; }
+      } else if (sc == S_STAT) {
+        if ((id == 1 || id == 2 || id == 5 || id == 6) && t == T_STRING) act = A_BIN;
+        else if ((id == 3 || id == 4) && t == T_I64) act = A_I64;
+      }
+      if (act == A_STRUCT) {
+        if (struct_begin()) return kTHRIFT;
+        if (child == S_DPH) h->has_dph = 1;
+        if (child == S_DICT) h->has_dict = 1;
+        if (child == S_V2) h->has_v2 = 1;
+        schs = (schs & ~(0xfu << (4 * depth))) | ((uint32_t)child << (4 * depth));
+        seen_up = (seen_up << 8) | (seen & 0xff);
+        seen = 0;
+        depth++;
+        continue;
+      }
+      int e;
+      if (act == A_I32) {
+        int32_t v = 0;
+        e = i32(&v);
+        seen |= bit;
+        if (!e) switch (slot) {  // a failed read leaves the field as it was  // 0-3 PageHeader, 4-7 DPH, 5-6 dictionary, 9-14 V2
+          case 0: h->type = v; break;
+          case 1: h->usize = v; break;
+          case 2: h->csize = v; break;
+          case 4: case 9: h->num_values = v; break;
+          case 5: case 12: h->encoding = v; break;
+          case 6: h->def_enc = v; break;
+          case 7: h->rep_enc = v; break;
+          case 13: h->v2_def_len = v; break;
+          case 14: h->v2_rep_len = v; break;
+          default: break;  // crc, num_nulls, num_rows
+        }
+      } else if (act == A_BOOL) {
+        bool b;
+        e = read_bool(&b);
+      } else if (act == A_I64) {
+        int64_t v;
+        e = i64(&v);
+      } else if (act == A_BIN) {
+        e = binary_skip();
+      } else {
+        // Skip(t): a primitive is read here; a container's frames are
+        // stepped by the loop (a failed start pushes no frame: error)
+        nf = 0;
+        se = start_value(t, 64, &nf);
+        if (se) return kTHRIFT;
+        skipping = nf > 0;
+        continue;
+      }
       if (e) return kTHRIFT;
     }
-    struct_end();
-    if (!st || !su || !sc) return kTHRIFT;  // "Required field ... is not set"
     h->hlen = (int32_t)(pos - start);
     return kOK;
-  }
-  PQG_TINLINE int read_dph(PageHdr* h) {
-    if (struct_begin()) return -1;
-    bool a = false, b = false, c = false, d = false;
-    for (;;) {
-      int t, id;
-      if (field_begin(&t, &id)) return -1;
-      if (t == T_STOP) break;
-      int e;
-      if (id == 1 && t == T_I32) { a = true; e = i32(&h->num_values); }
-      else if (id == 2 && t == T_I32) { b = true; e = i32(&h->encoding); }
-      else if (id == 3 && t == T_I32) { c = true; e = i32(&h->def_enc); }
-      else if (id == 4 && t == T_I32) { d = true; e = i32(&h->rep_enc); }
-      else if (id == 5 && t == T_STRUCT) e = read_statistics();
-      else e = skip(t, 64);
-      if (e) return -1;
-    }
-    struct_end();
-    return (a && b && c && d) ? 0 : -1;
-  }
-  PQG_TINLINE int read_dict(PageHdr* h) {
-    if (struct_begin()) return -1;
-    bool a = false, b = false;
-    for (;;) {
-      int t, id;
-      if (field_begin(&t, &id)) return -1;
-      if (t == T_STOP) break;
-      int e;
-      if (id == 1 && t == T_I32) { a = true; e = i32(&h->num_values); }
-      else if (id == 2 && t == T_I32) { b = true; e = i32(&h->encoding); }
-      else if (id == 3 && t == T_BOOL) { bool s; e = read_bool(&s); }
-      else e = skip(t, 64);
-      if (e) return -1;
-    }
-    struct_end();
-    return (a && b) ? 0 : -1;
-  }
-  PQG_TINLINE int read_v2(PageHdr* h) {
-    if (struct_begin()) return -1;
-    unsigned seen = 0;
-    for (;;) {
-      int t, id;
-      if (field_begin(&t, &id)) return -1;
-      if (t == T_STOP) break;
-      int e;
-      int32_t dummy;
-      if (id == 1 && t == T_I32) { seen |= 1; e = i32(&h->num_values); }
-      else if (id == 2 && t == T_I32) { seen |= 2; e = i32(&dummy); }
-      else if (id == 3 && t == T_I32) { seen |= 4; e = i32(&dummy); }
-      else if (id == 4 && t == T_I32) { seen |= 8; e = i32(&h->encoding); }
-      else if (id == 5 && t == T_I32) { seen |= 16; e = i32(&h->v2_def_len); }
-      else if (id == 6 && t == T_I32) { seen |= 32; e = i32(&h->v2_rep_len); }
-      else if (id == 7 && t == T_BOOL) { bool s; e = read_bool(&s); }  // IsCompressed: ignored (Q4)
-      else if (id == 8 && t == T_STRUCT) e = read_statistics();
-      else e = skip(t, 64);
-      if (e) return -1;
-    }
-    struct_end();
-    return seen == 63 ? 0 : -1;
   }
 };
 

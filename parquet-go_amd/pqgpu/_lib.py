@@ -35,6 +35,7 @@ def lib():
         "pqg_decode_chunks": ([P, C.POINTER(abi.ChunkJob), I, C.POINTER(abi.ChunkResult)], I),
         "pqg_get_pages": ([P, I, C.POINTER(abi.PageInfo), I], I),
         "pqg_last_timings": ([P, C.POINTER(C.c_float), I], I),
+        "pqg_set_timing": ([P, I], I),
         "pqg_debug_job": ([P, I, C.POINTER(I64), I], I),
         "pqg_debug_counters": ([P, C.POINTER(C.c_uint64), I], I),
         "pqg_bench_decode": ([P, C.POINTER(abi.ChunkJob), I, I, C.POINTER(C.c_float), C.POINTER(C.c_float), I], I),
@@ -67,7 +68,7 @@ def lib():
 EXPORTED = [
     "pqg_ctx_create", "pqg_ctx_destroy", "pqg_status_string", "pqg_device_alloc", "pqg_device_free",
     "pqg_memcpy_h2d", "pqg_memcpy_d2h", "pqg_decode_chunks_async", "pqg_sync", "pqg_decode_chunks",
-    "pqg_get_pages", "pqg_last_timings", "pqg_debug_job", "pqg_debug_counters", "pqg_bench_decode", "pqg_assemble",
+    "pqg_get_pages", "pqg_last_timings", "pqg_set_timing", "pqg_debug_job", "pqg_debug_counters", "pqg_bench_decode", "pqg_assemble",
     "pqg_assemble_list", "pqg_last_assemble_ms", "pqg_decode_page", "pqg_block_decompress", "pqg_pack_levels", "pqg_file_open", "pqg_file_open_tail",
     "pqg_file_close",
     "pqg_file_num_columns", "pqg_file_num_row_groups", "pqg_file_num_rows", "pqg_file_row_group_rows",

@@ -1,5 +1,6 @@
-"""Dictionary index streams walked inside k_dict4 (IdxWalk, pqg_dict.hip)
-against the oracle: hand-built dictionary chunks whose RLE_DICTIONARY pages
+"""Dictionary index streams of 4-byte dictionary pages on each decode path
+(run tables + k_dict4, the in-kernel walk IdxWalk, the fused level + index
+pass) against the oracle: hand-built dictionary chunks whose RLE_DICTIONARY pages
 carry index streams with run-level control at every bit width 1..32 -- RLE
 runs of 1 value to far past one batch, bit-packed runs of one group to
 hundreds (payload crossing the ring window), redundant varint header bytes
@@ -72,10 +73,27 @@ def dict_chunk(rng, pages, w, dcount, nullable=True, bad_frac=0.0, short_frac=0.
     return b"".join(parts)
 
 
-@pytest.fixture(scope="module")
-def dec():
+# the three decode paths of 4-byte dictionary pages (pqg_runtime.hip): run
+# tables + k_dict4 (default), the in-kernel walk (PQG_DICT_WALK=1) and the
+# fused level + index pass (PQG_FUSED=1); read when the context is created
+PATHS = {"tables": {}, "walk": {"PQG_DICT_WALK": "1"}, "fused": {"PQG_DICT_WALK": "1", "PQG_FUSED": "1"}}
+
+
+@pytest.fixture(scope="module", params=list(PATHS))
+def dec(request):
+    import os
     import pqgpu
-    d = pqgpu.GpuDecoder(0)
+    env = PATHS[request.param]
+    old = {k: os.environ.get(k) for k in ("PQG_DICT_WALK", "PQG_FUSED")}
+    os.environ.update(env)
+    try:
+        d = pqgpu.GpuDecoder(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     yield d
     d.close()
 

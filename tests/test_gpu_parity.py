@@ -233,6 +233,16 @@ def _hand_cases():
     t.b += bytes([0x1b, 0x01, 0x55, 0x02, 0x04])  # field 13 map<i32,i32> {1: 2}
     t.last[-1] = 13
     cases.append(("skip_fields", t.stop() + i32([9]), dict(ptype=abi.INT32)))
+    # a header whose unknown field is a LIST<STRUCT> of 2^30 elements at the end of
+    # the bytes: every element is an empty struct at EOF (skipped at once, not
+    # 2^30 times), then the header fails like the reference's
+    t = U.TW()
+    t.i32(1, 0).i32(2, 4).i32(3, 4)
+    cases.append(("huge_struct_list", t.b + bytes([0xA9, 0xFC]) + U.uvarint(1 << 30), dict(ptype=abi.INT32)))
+    t = U.TW()
+    t.i32(1, 0).i32(2, 4).i32(3, 4)
+    cases.append(("huge_struct_map", t.b + bytes([0xAB]) + U.uvarint(1 << 30) + bytes([0xC5]),
+                  dict(ptype=abi.INT32)))
     # INT96 truncated final value: left nil (Q8)
     cases.append(("int96_q8", U.v1_page(bytes(range(30)), 3, 0), dict(ptype=abi.INT96)))
     cases.append(("int96_short", U.v1_page(bytes(range(24)), 3, 0), dict(ptype=abi.INT96)))

@@ -10,7 +10,7 @@
 #   tests[:<pytest -k expr>]   pytest -m gpu (TESTS= files, default tests/)
 #   smoke                      __graft_entry__.smoke()
 #   bench[:<name>]             bench.py $BENCH_ARGS  -> bench_<name>.json
-#   only:<cfg>[:<name>]        bench.py --only <cfg> $ONLY_ARGS -> only_<name>.json
+#   only:<cfg>[:<name>[:<args>]]  bench.py --only <cfg> $ONLY_ARGS [args, commas for spaces] -> only_<name>.out
 #   probe:<cfg>                tools/probe_jobs.py --only <cfg> $PROBE_ARGS
 #   prof:<cfg>[:<name>[:<args>]]  rocprofv3 --kernel-trace --stats of bench.py --only <cfg> [args, commas
 #                              for spaces] -> prof_<name>.md
@@ -42,7 +42,10 @@ for step in "$@"; do
       rc=$?; tail -3 "$OUT/pytest.out" ;;
     smoke) run 300 smoke python -u -c "import __graft_entry__ as g; g.smoke()"; rc=$? ;;
     bench) run ${BENCH_TIMEOUT:-900} "bench_${a1:-main}" python -u bench.py $BENCH_ARGS; rc=$? ;;
-    only) run 400 "only_${a2:-$a1}" python -u bench.py --only "$a1" --steps "$STEPS_N" --warmup 2 $ONLY_ARGS; rc=$? ;;
+    only)  # only:<cfg>[:<name>[:<extra bench args, commas for spaces>]]
+      IFS=: read -r _k _c _n ex <<< "$step"
+      run 400 "only_${a2:-$a1}" python -u bench.py --only "$a1" --steps "$STEPS_N" --warmup 2 $ONLY_ARGS ${ex//,/ }
+      rc=$? ;;
     probe) run 400 "probe_$a1" python -u tools/probe_jobs.py --only "$a1" $PROBE_ARGS; rc=$? ;;
     prof)  # prof:<cfg>[:<name>[:<extra bench args, commas for spaces>]]
       nm=${a2:-$a1}

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     args = bench.argparse.Namespace(rows=a.rows, bits=a.bits, c1_rows=10_000_000, c3_rows=200_000_000,
-                                    c4_rows=50_000_000, c5_rows_per_rg=15_625_000)
+                                    c3gz_rows=50_000_000, c4_rows=50_000_000, c5_rows_per_rg=15_625_000)
     import pqgpu
     from pqgpu import abi
     dec = pqgpu.GpuDecoder(0)
