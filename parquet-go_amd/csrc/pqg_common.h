@@ -295,7 +295,8 @@ constexpr int kQueueLevLong = 13;  // pieces of the long level runs (k_level_lon
 constexpr int kQueueInflate = 14;  // GZIP pages (k_inflate)
 constexpr int kQueueDictWalk = 15;   // small 4-byte dictionary pages walked in-kernel, LDS dictionary (k_dict_walk)
 constexpr int kQueueDictWalkG = 16;  // the same, dictionary gathered from global memory (k_dict_walk_g)
-constexpr int kQueueSlots = 17;  // queue regions zeroed per launch: 0-8, the stage flags (9), 10-16
+constexpr int kQueueLevGen = 17;  // k_page_levels when k_page_levels_w1 takes the w = 1 jobs' pages
+constexpr int kQueueSlots = 18;  // queue regions zeroed per launch: 0-8, the stage flags (9), 10-16
 
 // Scan tiles of the speculative page-header search.
 constexpr int kScanTile = 16384;

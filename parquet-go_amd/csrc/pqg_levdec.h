@@ -159,10 +159,14 @@ __device__ int lrun_serial(const PQG_L uint8_t* win, uint32_t wo, uint32_t q, ui
   }
 }
 
-struct LevelDecoder {
+// kW1: a decoder for bit width 1 only (maxLevel 1: optional flat columns, the
+// C2 shape); the w > 1 expansion is not compiled in, so the kernel that uses
+// it needs fewer registers and runs more waves per SIMD.
+template <bool kW1>
+struct LevelDecoderT {
   gcu8 p;
   uint32_t n;      // stream bytes
-  int w;           // bit width (1..8)
+  int w;           // bit width (1..8; 1 when kW1)
   uint32_t count;  // values wanted
   gu8 out;         // count bytes
   uint32_t maxl;
@@ -497,7 +501,7 @@ struct LevelDecoder {
     m1 &= lm1;
     const bool b0 = (m0 >> lane) & 1, b1 = (m1 >> lane) & 1;
     const uint32_t pre = (uint32_t)(((uintptr_t)out + produced) & 15);
-    if (w == 1) {
+    if (kW1 || w == 1) {
       bits_clear();
       const bool hi = m1 != 0;
       const int ll = 63 - __builtin_clzll(hi ? m1 : m0);
@@ -514,6 +518,7 @@ struct LevelDecoder {
       if (total) bits_store(produced, total);
       return kOK;
     }
+    if constexpr (!kW1) {
     PQG_L uint8_t* TM = lds_ptr(sh->tmap);
     PQG_L u32x2_t* TE = lds_ptr(sh->tent);
     *(PQG_L u32x4_t*)(TM + 16 * lane) = u32x4_t{0u, 0u, 0u, 0u};
@@ -534,6 +539,7 @@ struct LevelDecoder {
                      (uint32_t)__builtin_amdgcn_readlane((int)(hi ? k1 : k0), ll);
     if (total > limit) total = limit;
     if (total) expand(produced, total);
+    }
     return kOK;
   }
 
@@ -631,7 +637,7 @@ struct LevelDecoder {
         if (!in_win(byte0, nbytes)) fill(byte0);
         info = 0x80000000u | (uint32_t)(((uint64_t)(byte0 - wbase) << 3) + (b0 & 7));
       }
-      if (w == 1) {
+      if (kW1 || w == 1) {
         // one dword of the piece per lane
         bits_clear();
         if ((uint32_t)lane <= (pre + piece - 1) >> 5) bits_or(pre, piece, bp, bp ? (info & 0x7fffffffu) : pay, lane);
@@ -640,6 +646,7 @@ struct LevelDecoder {
         done += piece;
         continue;
       }
+      if constexpr (!kW1) {
       PQG_L uint8_t* TM = lds_ptr(sh->tmap);
       *(PQG_L u32x4_t*)(TM + 16 * lane) = u32x4_t{0u, 0u, 0u, 0u};
       __builtin_amdgcn_wave_barrier();
@@ -651,6 +658,7 @@ struct LevelDecoder {
       expand(produced, piece);
       produced += piece;
       done += piece;
+      }
     }
     pos = nx;
     return kOK;
@@ -664,10 +672,14 @@ struct LongTables {
   int long_cap, piece_cap;
 };
 
+using LevelDecoder = LevelDecoderT<false>;
+
+template <bool kW1 = false>
 __device__ __forceinline__ int level_stream(gcu8 p, int64_t n, int w, uint32_t count, gu8 out, uint32_t maxl,
                                             LevShared& sh, uint32_t* nn, const LongTables& lt, int pidx,
                                             bool* deferred = nullptr) {
-  LevelDecoder dec{p, (uint32_t)n, w, count, out, maxl, &sh, lt.longs, lt.pieces, lt.ctr, lt.long_cap, lt.piece_cap, pidx};
+  LevelDecoderT<kW1> dec{p, (uint32_t)n, kW1 ? 1 : w, count, out, maxl, &sh, lt.longs, lt.pieces, lt.ctr, lt.long_cap,
+                         lt.piece_cap, pidx};
   const int e = dec.run();
 #ifdef PQG_PROFILE
   for (int k = 0; k < 8; k++) PQG_ACC(k, 0, dec.pacc[k]);

@@ -392,10 +392,17 @@ __global__ void __launch_bounds__(64) k_level_long(PageDev* pages, const int* ct
 // and dropped: with one lane per page a 35 000-page batch fills ~550 waves,
 // and each lane's serial walk of ~1 100 runs and 1 250 granules ran 4x slower
 // than this kernel: DESIGN.md.)
-__global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total,
-                                                    int* queue, uint8_t* scratch, HStream* streams,
-                                                    uint8_t* def_arena, uint8_t* rep_arena, LongLev* longs,
-                                                    int long_cap, LevPiece* pieces, int piece_cap) {
+// Two instances: k_page_levels_w1 for the pages of jobs whose levels are at
+// most 1 bit wide (maxR = 0, maxD <= 1: optional flat columns, required
+// columns) — the w = 1 decoder alone, 64 VGPRs and 8 waves per SIMD without
+// spills — and k_page_levels for every other page.  `split`: both kernels run
+// on one list, each taking its own jobs' pages (0: this kernel takes all).
+__device__ __forceinline__ bool w1_job(const JobDev& job) { return job.max_rep == 0 && job.max_def <= 1; }
+
+template <bool kW1>
+__device__ __forceinline__ void page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                                            uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena,
+                                            LongLev* longs, int long_cap, LevPiece* pieces, int piece_cap, int split) {
   __shared__ __attribute__((aligned(16))) LevShared sh;
   const int lane = lane_id();
   const LongTables lt{longs, pieces, const_cast<int*>(total), long_cap, piece_cap};
@@ -404,12 +411,13 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
     if (t >= *total) return;
     const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
     const PageDev pg = pages[pidx];
+    const JobDev job = jobs[pg.job];
+    if (split && w1_job(job) != kW1) continue;  // the other kernel's page
     if (lane == 0) {
       pages[pidx].hs_rep = pages[pidx].hs_def = pages[pidx].hs_val = -1;
       pages[pidx].vmode = -1;
     }
     if (pg.read_status != kOK || (pg.page_type != 0 && pg.page_type != 3)) continue;
-    const JobDev job = jobs[pg.job];
     if (job.status == kCAPACITY) continue;
     const PageStreams ps = page_setup(job, pg, pidx, pages, streams, total, scratch, lane == 0);
     if (ps.e != kOK) continue;
@@ -418,12 +426,12 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
     int64_t nn = 0;
     int de = kOK;
     if (n > 0) {
-      if (job.max_rep > 0) {
+      if (!kW1 && job.max_rep > 0) {
         if (ps.rep_n < 0) de = kLEVELS;  // V2 with no rep-level bytes: "reader is not initialized"
         else {
           uint32_t unused;
-          de = level_stream(ps.rep, ps.rep_n, bits_len((uint32_t)job.max_rep), (uint32_t)n,
-                            gmut(rep_arena) + job.slot_base + pg.slot_offset, 0x100u, sh, &unused, lt, pidx);
+          de = level_stream<kW1>(ps.rep, ps.rep_n, bits_len((uint32_t)job.max_rep), (uint32_t)n,
+                                 gmut(rep_arena) + job.slot_base + pg.slot_offset, 0x100u, sh, &unused, lt, pidx);
         }
       }
       if (de == kOK) {
@@ -431,9 +439,9 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
           if (ps.def_n < 0) de = kLEVELS;
           else {
             uint32_t c;
-            de = level_stream(ps.def, ps.def_n, bits_len((uint32_t)job.max_def), (uint32_t)n,
-                              gmut(def_arena) + job.slot_base + pg.slot_offset, (uint32_t)job.max_def, sh, &c, lt,
-                              pidx);
+            de = level_stream<kW1>(ps.def, ps.def_n, bits_len((uint32_t)job.max_def), (uint32_t)n,
+                                   gmut(def_arena) + job.slot_base + pg.slot_offset, (uint32_t)job.max_def, sh, &c, lt,
+                                   pidx);
             nn = c;
           }
         } else {
@@ -446,6 +454,26 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
       if (de != kOK) pages[pidx].decode_status = de;
     }
   }
+}
+
+__global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+                                                    int* queue, uint8_t* scratch, HStream* streams,
+                                                    uint8_t* def_arena, uint8_t* rep_arena, LongLev* longs,
+                                                    int long_cap, LevPiece* pieces, int piece_cap, int split) {
+  page_levels<false>(jobs, pages, list, total, queue, scratch, streams, def_arena, rep_arena, longs, long_cap, pieces,
+                     piece_cap, split);
+}
+
+#ifndef PQG_LEVELS_W1_WPE
+#define PQG_LEVELS_W1_WPE 8
+#endif
+__global__ void __launch_bounds__(64, PQG_LEVELS_W1_WPE) k_page_levels_w1(JobDev* jobs, PageDev* pages, const int* list,
+                                                       const int* total, int* queue, uint8_t* scratch,
+                                                       HStream* streams, uint8_t* def_arena, uint8_t* rep_arena,
+                                                       LongLev* longs, int long_cap, LevPiece* pieces, int piece_cap,
+                                                       int split) {
+  page_levels<true>(jobs, pages, list, total, queue, scratch, streams, def_arena, rep_arena, longs, long_cap, pieces,
+                    piece_cap, split);
 }
 
 // ---- K3d ---------------------------------------------------------------------

@@ -56,7 +56,10 @@ __global__ void k_snap_decode(const JobDev* jobs, PageDev* pages, const SnapSub*
                               int sub_cap, int* queue, uint8_t* scratch);
 __global__ void k_page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                               uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena,
-                              LongLev* longs, int long_cap, LevPiece* pieces, int piece_cap);
+                              LongLev* longs, int long_cap, LevPiece* pieces, int piece_cap, int split);
+__global__ void k_page_levels_w1(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                              uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena,
+                              LongLev* longs, int long_cap, LevPiece* pieces, int piece_cap, int split);
 __global__ void k_dict_resolve(JobDev* jobs, int n_jobs, PageDev* pages, uint8_t* scratch);
 __global__ void k_page_fused(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                              uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena, LongLev* longs,
@@ -592,8 +595,22 @@ static int launch_pipeline(pqg_ctx* c) {
                        ctr, Q(1), scratch, streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p, llong, llc,
                        lpieces, lpc, (uint8_t*)c->value_arena.p, (uint64_t*)c->lookback.p);
   } else {
-    hipLaunchKernelGGL(k_page_levels, dim3(qgrid(c->num_cus * 24)), dim3(64), 0, s, jobs, pages, list, ctr, Q(1), scratch,
-                       streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p, llong, llc, lpieces, lpc);
+    // pages of jobs with 1-bit levels (maxR = 0, maxD <= 1) to the w = 1
+    // decoder, the others to the general one; a kernel with no job stays idle
+    bool any_w1 = false, any_gen = false;
+    for (int i = 0; i < n; i++) {
+      const pqg_column_desc& d = c->cur[(size_t)i].col;
+      (d.max_rep == 0 && d.max_def <= 1 ? any_w1 : any_gen) = true;
+    }
+    const int split = any_w1 && any_gen;
+    if (any_w1)
+      hipLaunchKernelGGL(k_page_levels_w1, dim3(qgrid(c->num_cus * 32)), dim3(64), 0, s, jobs, pages, list, ctr, Q(1),
+                         scratch, streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p, llong, llc, lpieces, lpc,
+                         split);
+    if (any_gen)
+      hipLaunchKernelGGL(k_page_levels, dim3(qgrid(c->num_cus * 24)), dim3(64), 0, s, jobs, pages, list, ctr,
+                         Q(split ? kQueueLevGen : 1), scratch, streams, (uint8_t*)c->def_arena.p,
+                         (uint8_t*)c->rep_arena.p, llong, llc, lpieces, lpc, split);
   }
   hipLaunchKernelGGL(k_level_long, dim3(qgrid(c->num_cus * 8)), dim3(64), 0, s, pages, ctr, llong, llc, lpieces, lpc,
                      Q(kQueueLevLong));
