@@ -60,18 +60,24 @@ struct PieceShared {
   uint8_t rmap[kHBlock];            // run starting at each value of a multi-run block
   uint8_t ridx[kHBlock];            // run of each value of a multi-run block
 };
-// LDS of a dictionary workgroup.  kMode 0: run-table pages (k_dict4); 1:
-// walked pages with a dictionary of <= kDictLdsEntries entries (k_dict_walk);
-// 2: walked pages gathering from global memory (k_dict_walk_g: no LDS
-// dictionary, so more workgroups fit a CU).
+// LDS of a dictionary workgroup.  kMode 0: run-table pages with a dictionary
+// of <= kDictLdsEntries entries, or none (k_dict4); 3: run-table pages with a
+// larger dictionary, its first kBigLdsEntries entries in LDS (k_dict4_big, one
+// 8-wave workgroup per CU); 1: walked pages with a dictionary of <=
+// kDictLdsEntries entries (k_dict_walk); 2: walked pages gathering from global
+// memory (k_dict_walk_g: no LDS dictionary, so more workgroups fit a CU).
+constexpr int kBigWaves = 8;
+constexpr int kBigLdsEntries = 26624;  // 104 KiB: with 8 waves' page stages, one workgroup per CU
+template <int kMode>
+constexpr int dict_waves() { return kMode == 3 ? kBigWaves : kDWaves; }
 template <int kMode>
 struct DictShared {
-  uint32_t dict[kMode == 2 ? 1 : kDictLdsEntries];
-  typename std::conditional<kMode == 0, PieceShared, WalkShared>::type w[kDWaves];
+  uint32_t dict[kMode == 2 ? 1 : kMode == 3 ? kBigLdsEntries : kDictLdsEntries];
+  typename std::conditional<kMode == 0 || kMode == 3, PieceShared, WalkShared>::type w[dict_waves<kMode>()];
   const uint8_t* dict_ptr;          // the dictionary being staged (set by a wave that holds its VRec)
   int dict_cnt;
   int item;
-  int wjob[kDWaves];                // job of each wave's page (-1: none, or done)
+  int wjob[dict_waves<kMode>()];    // job of each wave's page (-1: none, or done)
   int dict_job;                     // job whose dictionary `dict` holds (-1: none)
 };
 
@@ -302,6 +308,14 @@ __device__ __forceinline__ int64_t dict_page(PieceShared& ps, const gcu8 sp, con
   return bad;
 }
 
+// a run-table page for k_dict4_big: a dictionary past the small LDS size of
+// which the LDS prefix holds at least a third (C2 b = 16: 0.39 -> 0.31 ms;
+// b = 20's 1 M entries gain nothing from 2.5 % and lose the occupancy, 0.55 ->
+// 0.65 ms, so they stay with k_dict4's global gathers)
+__device__ __forceinline__ bool big_dict(const VRec& r) {
+  return r.dict && r.dcount > kDictLdsEntries && r.dcount <= 3 * kBigLdsEntries;
+}
+
 // Read phase of every 4-byte dictionary page in the list, and its VRec at the
 // page's list position (valuesDecoder.init type_dict.go:22-37: the bit-width
 // byte, > 32 is an error).
@@ -365,6 +379,7 @@ __global__ void __launch_bounds__(256) k_dict_plan(JobDev* jobs, PageDev* pages,
             r.out = value_arena + J.value_base + (P.value_offset + pr.v0) * 4;
             r.produced = S.produced;
             r.serr = (S.status != kOK && S.produced < r.nn) ? S.status : kOK;
+            if (big_dict(r)) const_cast<int*>(total)[kModePresentOff + kPresentBigDict] = 1;
           }
         }
       }
@@ -400,10 +415,13 @@ __device__ __forceinline__ int walk_dict_page(VRec& r, WalkShared& ws, const Dic
 }
 
 template <int kMode>
-__device__ __forceinline__ void dict_items(PageDev* pages, const int* total, int* queue, const VRec* recs) {
+__device__ __forceinline__ void dict_items(PageDev* pages, const int* total, int* queue, const VRec* recs,
+                                           int big = 0) {
   __shared__ __attribute__((aligned(16))) DictShared<kMode> sh;
+  constexpr int kDWaves = dict_waves<kMode>();  // this kernel's waves per workgroup (= pages per item)
   const int lane = lane_id(), wid = (int)(threadIdx.x >> 6);
   if (total[kModePresentOff + 1] == 0) return;  // no page of this stage
+  if (kMode == 3 && total[kModePresentOff + kPresentBigDict] == 0) return;
   if (threadIdx.x == 0) sh.dict_job = -1;
   const int nt = min(total[kCtrItems], total[kCtrPartsCap]);  // work items: pages' parts (k_part_plan)
   DProf pf;
@@ -418,7 +436,10 @@ __device__ __forceinline__ void dict_items(PageDev* pages, const int* total, int
     VRec r;
     r.job = -1;
     if (t < nt) r = recs[t];
-    const int own = kMode == 0 ? (r.n_blocks >= 0) : kMode == 1 ? (r.n_blocks == -1) : (r.n_blocks == -2);
+    const int own = kMode == 0   ? (r.n_blocks >= 0 && !(big && big_dict(r)))
+                    : kMode == 3 ? (r.n_blocks >= 0 && big_dict(r))
+                    : kMode == 1 ? (r.n_blocks == -1)
+                                 : (r.n_blocks == -2);
     if (!own) r.job = -1;  // another kernel's page
     PQG_DT(t1);
     pf.add(2, t1 - t0);
@@ -458,7 +479,26 @@ __device__ __forceinline__ void dict_items(PageDev* pages, const int* total, int
         }
         __syncthreads();
         const int64_t dc = sh.dict_ptr ? sh.dict_cnt : 0;
-        if (dc > 0 && dc <= kDictLdsEntries) {
+        if constexpr (kMode == 3) {
+          // the dictionary's first kBigLdsEntries entries, in rounds of 8 loads per thread
+          const PQG_G uint32_t* src = (const PQG_G uint32_t*)gconst(sh.dict_ptr);
+          const int m = (int)(dc < kBigLdsEntries ? dc : kBigLdsEntries);
+          for (int b0 = 0; b0 < m; b0 += 8 * kDWaves * 64) {
+            uint32_t rr[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+              const int i = b0 + (int)threadIdx.x + k * kDWaves * 64;
+              rr[k] = src[i < m ? i : 0];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+              const int i = b0 + (int)threadIdx.x + k * kDWaves * 64;
+              if (i < m) sh.dict[i] = rr[k];
+            }
+          }
+          __syncthreads();
+          if (threadIdx.x == 0) sh.dict_job = want;
+        } else if (dc > 0 && dc <= kDictLdsEntries) {
           const PQG_G uint32_t* src = (const PQG_G uint32_t*)gconst(sh.dict_ptr);
           uint32_t rr[kDictLdsEntries / (kDWaves * 64)];
 #pragma unroll
@@ -489,6 +529,16 @@ __device__ __forceinline__ void dict_items(PageDev* pages, const int* total, int
         } else if constexpr (kMode == 1) {
           // k_dict_plan gives this kernel only pages whose dictionary fits LDS
           de = lds ? walk_dict_page(r, sh.w[wid], LdsDict{lds_ptr(sh.dict)}) : kCAPACITY;
+        } else if constexpr (kMode == 3) {
+          PieceShared& ps = sh.w[wid];
+          const PQG_G uint32_t* dg = (const PQG_G uint32_t*)gconst(r.dict);
+          const uint32_t nl = (uint32_t)(r.dcount < kBigLdsEntries ? r.dcount : kBigLdsEntries);
+          int64_t bad = dict_page(ps, gconst(r.p), r.n, r.w, gconst(r.runs), gconst(r.blks), r.n_blocks,
+                                  (uint32_t)r.count, gmut(r.out), (uint32_t)r.dcount,
+                                  PrefixDict{lds_ptr(sh.dict), dg, lds ? nl : 0u}, pf);
+          bad = wave_min(bad);
+          if (bad < r.nn && (r.serr == kOK || bad < r.produced)) de = kDICT_INDEX;
+          else de = r.serr;
         } else if constexpr (kMode == 0) {
           const gcu8 sp = gconst(r.p);
           const PQG_G RunEnt* rt = gconst(r.runs);
@@ -524,9 +574,14 @@ __device__ __forceinline__ void dict_items(PageDev* pages, const int* total, int
   pf.flush();
 }
 
+// big: k_dict4_big runs too and takes the pages with larger dictionaries
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, kDWaves * 64), amdgpu_waves_per_eu(PQG_DICT_WPE)))
-k_dict4(PageDev* pages, const int* total, int* queue, const VRec* recs) {
-  dict_items<0>(pages, total, queue, recs);
+k_dict4(PageDev* pages, const int* total, int* queue, const VRec* recs, int big) {
+  dict_items<0>(pages, total, queue, recs, big);
+}
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, kBigWaves * 64), amdgpu_waves_per_eu(2)))
+k_dict4_big(PageDev* pages, const int* total, int* queue, const VRec* recs) {
+  dict_items<3>(pages, total, queue, recs, 1);
 }
 
 #ifndef PQG_DICT_WALK_WPE

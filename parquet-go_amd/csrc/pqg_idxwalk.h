@@ -68,6 +68,22 @@ struct GlobalDict {
   const PQG_G uint32_t* d;
   __device__ __forceinline__ uint32_t operator()(uint32_t k) const { return d[k]; }
 };
+// A dictionary whose first n entries are in LDS and the rest in global memory
+// (k_dict4_big).  Both loads are issued for every lane (a load under a branch
+// is waited for inside it); lanes served by LDS all read global entry 0, one
+// request per wave, so only the keys past the prefix cost L2 requests.
+struct PrefixDict {
+  static constexpr bool kGlobal = true;
+  const PQG_L uint32_t* l;
+  const PQG_G uint32_t* g;
+  uint32_t n;
+  __device__ __forceinline__ uint32_t operator()(uint32_t k) const {
+    const bool in = k < n;
+    const uint32_t gv = g[in ? 0u : k];
+    const uint32_t lv = l[in ? k : 0u];
+    return in ? lv : gv;
+  }
+};
 
 // ---- Small pages: the index stream walked here, wave-parallel ----------------
 // hybridDecoder.next (hybrid_decoder.go:82-166) over a page's keys without the

@@ -77,7 +77,9 @@ __global__ void k_values(JobDev* jobs, PageDev* pages, const PartRec* parts, con
 __global__ void k_dict_plan(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total,
                             uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks,
                             VRec* recs, int walk_small);
-__global__ void k_dict4(PageDev* pages, const int* total, int* queue, const VRec* recs);
+__global__ void k_dict4(PageDev* pages, const int* total, int* queue, const VRec* recs, int big);
+__global__ void k_dict4_big(PageDev* pages, const int* total, int* queue, const VRec* recs);
+constexpr int kBigDictThreads = 512;
 __global__ void k_dict_walk(PageDev* pages, const int* total, int* queue, const VRec* recs);
 __global__ void k_dict_walk_g(PageDev* pages, const int* total, int* queue, const VRec* recs);
 __global__ void k_finalize(JobDev* jobs, int n_jobs, PageDev* pages);
@@ -186,6 +188,7 @@ struct pqg_ctx {
   bool dict4 = true;     // k_dict4 for 4-byte dictionary pages (PQG_DICT4=0: k_values<1>, for A/B runs)
   // Measured alternatives, off by default (C2 on one MI355X, r05_s8: run tables
   // 3.15 ms/step, in-kernel walk 3.33, fused 3.86):
+  bool dict_big = true;   // k_dict4_big for dictionaries past 4096 entries (PQG_DICT_BIG=0: k_dict4 gathers them)
   bool dict_walk = false; // PQG_DICT_WALK=1: k_dict_walk / k_dict_walk_g walk small pages' index streams themselves
   bool fused = false;     // PQG_FUSED=1: k_page_fused, levels + small 4-byte dictionary pages in one pass
   DevBuf lookback;       // k_page_fused: one look-back word per page
@@ -274,6 +277,7 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
   for (auto& e : c->ev_k8) hipEventCreate(&e);
   if (const char* e = getenv("PQG_DICT4")) c->dict4 = atoi(e) != 0;
   if (const char* e = getenv("PQG_DICT_WALK")) c->dict_walk = atoi(e) != 0;
+  if (const char* e = getenv("PQG_DICT_BIG")) c->dict_big = atoi(e) != 0;
   if (const char* e = getenv("PQG_FUSED")) c->fused = atoi(e) != 0;
   {
     hipFuncAttributes fa;
@@ -636,8 +640,13 @@ static int launch_pipeline(pqg_ctx* c) {
     hipLaunchKernelGGL(k_dict_plan, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((items_cap + 255) / 256, c->num_cus * 4))),
                        dim3(256), 0, s, jobs, pages, parts, ctr, (uint8_t*)c->value_arena.p, streams, runs, blks, recs,
                        walk_small);
+    // dictionaries past 4096 entries: k_dict4_big (a 104 KiB LDS prefix, one
+    // 8-wave workgroup per CU) takes their run-table pages (PQG_DICT_BIG=0: k_dict4)
     hipLaunchKernelGGL(k_dict4, dim3(qgrid(c->num_cus * c->dict4_per_cu)), dim3(c->dict4_threads), 0, s, pages, ctr, Q(3),
-                       recs);
+                       recs, (int)c->dict_big);
+    if (c->dict_big)
+      hipLaunchKernelGGL(k_dict4_big, dim3(qgrid(c->num_cus)), dim3(kBigDictThreads), 0, s, pages, ctr,
+                         Q(kQueueDictBig), recs);
     if (walk_small) {
       hipLaunchKernelGGL(k_dict_walk, dim3(qgrid(c->num_cus * c->dict_walk_per_cu)), dim3(c->dict4_threads), 0, s, pages,
                          ctr, Q(kQueueDictWalk), recs);
