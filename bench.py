@@ -169,8 +169,9 @@ def _level_sections(pf, meta, pg, desc):
     return pos, pg.uncompressed_size - pos
 
 
-def account(wl, dec, res):
-    """B_in/B_out of the step and algorithmic bytes per stage."""
+def account(wl, pages_of, res):
+    """B_in/B_out of the step and algorithmic bytes per stage.
+    pages_of(ji): the page records of job ji (from the context that decoded it)."""
     b_in = b_out = 0
     st = dict.fromkeys(STAGES, 0)
     ji = 0
@@ -190,7 +191,7 @@ def account(wl, dec, res):
                 b_out += r.values_bytes + (r.num_values + 1) * 4 + slots_out
             st["scan"] += meta.total_compressed_size
             lev_in = val_in = dict_in = 0
-            for pg in dec.pages(ji):
+            for pg in pages_of(ji):
                 if pg.page_type == 2:
                     dict_in += pg.uncompressed_size
                     continue
@@ -326,7 +327,24 @@ def pmc_traffic(key, kernels, workload):
 
 
 # ---------------------------------------------------------------- run one workload
-def run_workload(wl, dec, args, steps, warmup, barrier, dist, world, rank, cpu_seconds):
+def split_jobs(jobs, k):
+    """Jobs dealt to k decode contexts, largest first to the least loaded
+    (by TotalCompressedSize): [(context, [job indices])]."""
+    load = [0] * k
+    parts = [[] for _ in range(k)]
+    for i in sorted(range(len(jobs)), key=lambda i: -jobs[i].total_compressed_size):
+        c = min(range(k), key=lambda c: load[c])
+        parts[c].append(i)
+        load[c] += jobs[i].total_compressed_size
+    return [sorted(p) for p in parts if p]
+
+
+def run_workload(wl, decs, args, steps, warmup, barrier, dist, world, rank, cpu_seconds):
+    """One workload's line.  decs: the decode contexts (each with its own HIP
+    stream); the chunks are dealt over them and decoded concurrently
+    (pqg_decode_chunks_async on each, then pqg_sync on each), so one
+    context's level stage overlaps another's values stage."""
+    dec = decs[0]
     import pqgpu
     from pqgpu import abi
     L = dec.L
@@ -339,33 +357,56 @@ def run_workload(wl, dec, args, steps, warmup, barrier, dist, world, rank, cpu_s
         wl.uploaded += nbytes
         jobs += fj
     n = len(jobs)
-    arr = (abi.ChunkJob * n)(*jobs)
-    res = (abi.ChunkResult * n)()
+    parts = split_jobs(jobs, max(1, min(len(decs), n)))
+    K = len(parts)
+    arrs = [(abi.ChunkJob * len(p))(*[jobs[i] for i in p]) for p in parts]
+    ress = [(abi.ChunkResult * len(p))() for p in parts]
+    where = {i: (c, j) for c, p in enumerate(parts) for j, i in enumerate(p)}
     tmp = (C.c_float * 16)()
 
     def step():
-        rc = L.pqg_decode_chunks(dec.ctx, arr, n, res)
-        if rc != 0:
-            raise RuntimeError("decode failed: %d" % rc)
+        for c in range(K):
+            rc = L.pqg_decode_chunks_async(decs[c].ctx, arrs[c], len(parts[c]))
+            if rc != 0:
+                raise RuntimeError("decode failed: %d" % rc)
+        for c in range(K):
+            rc = L.pqg_sync(decs[c].ctx, ress[c], len(parts[c]))
+            if rc != 0:
+                raise RuntimeError("decode failed: %d" % rc)
+
+    def set_timing(on):
+        for c in range(K):
+            L.pqg_set_timing(decs[c].ctx, on)
 
     for _ in range(max(warmup, 1)):
         step()
+    res = (abi.ChunkResult * n)()
+    for i, (c, j) in where.items():
+        res[i] = ress[c][j]
     bad = [abi.status_name(res[i].status) for i in range(n) if res[i].status != 0]
     assert not bad, "%s: %s" % (wl.key, bad)
     # the timed steps run without the per-stage HIP events (instrumentation,
-    # a few us of stream time each); the stage breakdown comes from as many
-    # instrumented steps after them
-    L.pqg_set_timing(dec.ctx, 0)
+    # a few us of stream time each).  The stage breakdown and the roofline come
+    # from as many instrumented steps after them on ONE context (all chunks,
+    # one stream): each kernel alone on the GPU, so its launch duration is its
+    # own (with K streams the stages of different contexts share the GPU and
+    # every launch stretches).  rocprofv3 summaries of `--streams 1` runs agree
+    # with these durations.
+    set_timing(0)
     barrier()
     t_start = time.perf_counter()
     for _ in range(steps):
         step()
     t_end = time.perf_counter()
     barrier()
+    arr1 = (abi.ChunkJob * n)(*jobs)
+    res1 = (abi.ChunkResult * n)()
     L.pqg_set_timing(dec.ctx, 1)
     stage_acc = np.zeros(len(STAGES))
     for _ in range(steps):
-        step()
+        rc = L.pqg_decode_chunks(dec.ctx, arr1, n, res1)
+        if rc != 0:
+            raise RuntimeError("decode failed: %d" % rc)
         k = L.pqg_last_timings(dec.ctx, tmp, 16)
         stage_acc += np.array([tmp[i] for i in range(1, min(k, 1 + len(STAGES)))])
     elapsed = t_end - t_start
@@ -375,7 +416,7 @@ def run_workload(wl, dec, args, steps, warmup, barrier, dist, world, rank, cpu_s
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    b_in, b_out, alg = account(wl, dec, res)
+    b_in, b_out, alg = account(wl, dec.pages, res1)
     stage_ms = stage_acc / steps
     dev_ms = float(stage_ms.sum())
     dom = int(np.argmax(stage_ms))
@@ -401,11 +442,13 @@ def run_workload(wl, dec, args, steps, warmup, barrier, dist, world, rank, cpu_s
             "traffic": pmc_traffic(wl.key, STAGE_KERNELS[dom_name], wl.desc),
             "alg_bytes_per_launch": alg[dom_name],
             "kernel_ms": round(float(stage_ms[dom]), 4),
+            "measured_on": "one context (all chunks on one stream), instrumented steps after the timed ones",
             "pipeline_device_ms": round(dev_ms, 4),
             "pipeline_frac": round((b_in + b_out) / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dev_ms else 0.0,
             "stage_ms": {s: round(float(x), 4) for s, x in zip(STAGES, stage_ms)},
             "stage_alg_bytes": alg,
         },
+        "streams": K,
     }
     if not args.no_verify:
         out["verified_bit_exact"] = verify(wl, dec, res)
@@ -525,6 +568,7 @@ def main():
     ap.add_argument("--c3gz-rows", type=int, default=50_000_000)
     ap.add_argument("--c4-rows", type=int, default=50_000_000)
     ap.add_argument("--c5-rows-per-rg", type=int, default=15_625_000)
+    ap.add_argument("--streams", type=int, default=2, help="decode contexts (HIP streams) the chunks are dealt over")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=16.0, help="bound on the headline CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -558,7 +602,9 @@ def main():
             dist.barrier()
 
     import pqgpu
-    dec = pqgpu.GpuDecoder(device)
+    # decode contexts, one HIP stream each (run_workload deals the chunks over them)
+    decs = [pqgpu.GpuDecoder(device) for _ in range(max(1, args.streams))]
+    dec = decs[0]
 
     def release(wl):
         for d in wl.devs:
@@ -567,22 +613,23 @@ def main():
 
     if args.only:  # profiling runs (tools/gpu_profile.sh): one workload, its own JSON line
         w = gen_workload(args.only, args, rank, world)
-        sub, _ = run_workload(w, dec, args, args.steps, args.warmup, barrier, dist, world, rank, 6.0)
+        sub, _ = run_workload(w, decs, args, args.steps, args.warmup, barrier, dist, world, rank, 6.0)
         if rank == 0:
             print(json.dumps({"only": args.only, "n_gpus": world, **sub}), flush=True)
         release(w)
-        dec.close()
+        for d in decs:
+            d.close()
         return
 
     wl = gen_workload("c2", args, rank, world)
-    head, res = run_workload(wl, dec, args, args.steps, args.warmup, barrier, dist, world, rank, args.cpu_seconds)
+    head, res = run_workload(wl, decs, args, args.steps, args.warmup, barrier, dist, world, rank, args.cpu_seconds)
     k8 = k8_c2(dec, wl, res, args) if rank == 0 else None
     release(wl)
     del wl
     subs = {}
     for key in [k for k in args.configs.split(",") if k]:
         w = gen_workload(key, args, rank, world)
-        sub, sres = run_workload(w, dec, args, args.sub_steps, 1, barrier, dist, world, rank, 6.0)
+        sub, sres = run_workload(w, decs, args, args.sub_steps, 1, barrier, dist, world, rank, 6.0)
         if key == "c5" and rank == 0:
             sub["k8_list_export"] = k8_list_c5(dec, w, sres, args)
         subs[key + ("_shard" if key == "c5" else "")] = sub
@@ -608,6 +655,7 @@ def main():
                 "chunks_per_step": head["chunks_per_step"],
                 "bytes_in": head["bytes_in"],
                 "bytes_out": head["bytes_out"],
+                "streams": head["streams"],
                 "parallelism": ("row-group shards: one process per GPU, RG i -> GPU floor(i*N/R), no data-path "
                                 "collective" if world > 1 else "single GPU"),
             },
@@ -619,7 +667,8 @@ def main():
             "configs": subs,
         }
         print(json.dumps(out), flush=True)
-    dec.close()
+    for d in decs:
+        d.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -49,7 +49,10 @@ int prof_read_levels(unsigned long long* out) {
 // one lane per stream: small blocks spread the (latency-bound) lanes over
 // every CU instead of one 256-lane block on each of the first few
 
-constexpr int kLaneWinG = 8;  // 16-byte granules of a lane's window (128 bytes)
+#ifndef PQG_LANE_WIN
+#define PQG_LANE_WIN 8
+#endif
+constexpr int kLaneWinG = PQG_LANE_WIN;  // 16-byte granules of a lane's window (128 bytes)
 struct LaneWin {
   gcu8 p;
   uint32_t n;

@@ -221,6 +221,8 @@ struct pqg_ctx {
   int launches = 0;                     // pipeline launches of the last decode
   bool any_var = false;                 // batch holds variable-length columns
   bool any_fixed_other = false;         // batch holds fixed-width columns (k_values<0> pages possible)
+  bool any_w4 = false;                  // batch holds 4-byte columns (the 4-byte dictionary stage: mode 1 pages)
+  bool any_levels = false;              // batch holds columns with levels (long level runs possible)
   int n_jobs = 0;
   int64_t list_cap = 0;
   hipEvent_t ev[kStages + 1];
@@ -616,8 +618,11 @@ static int launch_pipeline(pqg_ctx* c) {
                          Q(split ? kQueueLevGen : 1), scratch, streams, (uint8_t*)c->def_arena.p,
                          (uint8_t*)c->rep_arena.p, llong, llc, lpieces, lpc, split);
   }
-  hipLaunchKernelGGL(k_level_long, dim3(qgrid(c->num_cus * 8)), dim3(64), 0, s, pages, ctr, llong, llc, lpieces, lpc,
-                     Q(kQueueLevLong));
+  // stages with no possible work are not launched (the host knows each job's
+  // type and levels; the kernels' own flags stay as the backstop)
+  if (c->any_levels)
+    hipLaunchKernelGGL(k_level_long, dim3(qgrid(c->num_cus * 8)), dim3(64), 0, s, pages, ctr, llong, llc, lpieces, lpc,
+                       Q(kQueueLevLong));
   if (c->timed) hipEventRecord(c->ev[4], s);
   const unsigned walk_blocks = (unsigned)std::max<int64_t>(
       1, std::min<int64_t>((c->list_cap + kWalkLanes - 1) / kWalkLanes, c->num_cus * (2048 / kWalkLanes)));
@@ -635,7 +640,9 @@ static int launch_pipeline(pqg_ctx* c) {
   // every values kernel takes the work items (the pages' parts) and keeps the
   // ones whose vmode (set by k_page_levels) is its own
   const int64_t items_cap = c->parts_cap;
-  if (c->dict4) {  // 4-byte dictionary pages: pieces staged in LDS, small dictionaries in LDS (pqg_dict.hip)
+  if (!c->any_w4) {
+    // no 4-byte column: no mode 1 page
+  } else if (c->dict4) {  // 4-byte dictionary pages: pieces staged in LDS, small dictionaries in LDS (pqg_dict.hip)
     VRec* recs = (VRec*)c->vrecs.p;
     hipLaunchKernelGGL(k_dict_plan, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((items_cap + 255) / 256, c->num_cus * 4))),
                        dim3(256), 0, s, jobs, pages, parts, ctr, (uint8_t*)c->value_arena.p, streams, runs, blks, recs,
@@ -699,6 +706,8 @@ int pqg_decode_chunks_async(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs) {
   c->force.assign((size_t)n_jobs, Caps());
   c->any_var = false;
   c->any_fixed_other = false;
+  c->any_w4 = false;
+  c->any_levels = false;
   c->prewalk = false;
   for (int i = 0; i < n_jobs; i++) {
     const JobKey key{(uintptr_t)jobs[i].data, jobs[i].total_compressed_size, jobs[i].num_values_hint};
@@ -709,6 +718,8 @@ int pqg_decode_chunks_async(pqg_ctx* c, const pqg_chunk_job* jobs, int n_jobs) {
     c->any_var |= value_width_of(jobs[i].col) == 0 || jobs[i].col.physical_type == PQG_FIXED_LEN_BYTE_ARRAY;
     // k_values<0>: every fixed-width column but 4-byte ones with only dictionary pages
     c->any_fixed_other |= value_width_of(jobs[i].col) != 0;
+    c->any_w4 |= value_width_of(jobs[i].col) == 4;
+    c->any_levels |= jobs[i].col.max_def > 0 || jobs[i].col.max_rep > 0;
   }
   if (n_jobs == 0) return PQG_OK;
   int e = plan_batch(c);
