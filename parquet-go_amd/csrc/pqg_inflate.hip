@@ -101,7 +101,7 @@ struct Inflater {
   uint32_t crc = 0;     // CRC-32 of the member's flushed bytes (conditioned)
   int lane;
 
-  __device__ void stage(int64_t at) {
+  __device__ __forceinline__ void stage(int64_t at) {
     // 16-byte granules from the aligned address at or below `at`; granules
     // past the block re-read its last one (never used)
     const uintptr_t a0 = (uintptr_t)(src + at) & ~(uintptr_t)15;
@@ -117,13 +117,26 @@ struct Inflater {
     if (i < in_base || i >= in_base + kInStage) stage(i);
     return lds_ptr(sh->in)[i - in_base];
   }
-  // at least k (<= 32) bits in the buffer; false past the end of the block
+  // the 4 bytes at i (staged window; bytes past the block are never used)
+  __device__ __forceinline__ uint32_t word_at(int64_t i) {
+    if (i < in_base || i + 4 > in_base + kInStage) stage(i);
+    const uint32_t o = (uint32_t)(i - in_base);
+    const PQG_L uint32_t* W = (const PQG_L uint32_t*)lds_ptr(sh->in);
+    return __builtin_amdgcn_alignbit(W[(o >> 2) + 1], W[o >> 2], (o & 3) * 8);
+  }
+  // at least k (<= 32) bits in the buffer; false past the end of the block.
+  // Whole bytes are taken up to 4 at a time (one LDS read per refill, not one
+  // per byte): the buffer runs ahead of the decode, which only ever reads it.
   __device__ __forceinline__ bool need(int k) {
     while (bitcnt < k) {
       if (pos >= n) return false;
-      bitbuf |= (uint64_t)(uint32_t)byte_at(pos) << bitcnt;
-      pos++;
-      bitcnt += 8;
+      int m = (64 - bitcnt) >> 3;
+      m = m > 4 ? 4 : m;
+      if ((int64_t)m > n - pos) m = (int)(n - pos);
+      const uint32_t x = word_at(pos);
+      bitbuf |= (uint64_t)(m >= 4 ? x : (x & ((1u << (8 * m)) - 1))) << bitcnt;
+      pos += m;
+      bitcnt += 8 * m;
     }
     return true;
   }
@@ -147,7 +160,7 @@ struct Inflater {
   // the 9-bit fast table.  Returns the number of unused code points at the
   // longest length (< 0: over-subscribed, 0: complete, > 0: incomplete), as
   // puff's construct.
-  __device__ int build(Huff& h, const uint16_t* lengths, int nsym) {
+  __device__ __forceinline__ int build(Huff& h, const uint16_t* lengths, int nsym) {
     PQG_L Huff* H = lds_ptr(&h);
     // counts (every lane, the same: n <= 288, cheap next to the block's symbols)
     uint32_t cnt[16];
@@ -230,7 +243,7 @@ struct Inflater {
   }
 
   // ---- output: the history ring, flushed to HBM (bytes below cap) and CRC'd
-  __device__ void flush_to(int64_t upto) {
+  __device__ __forceinline__ void flush_to(int64_t upto) {
     PQG_L uint8_t* ring = lds_ptr(sh->ring);
     __builtin_amdgcn_wave_barrier();
     const int64_t nb = upto - flushed;
@@ -286,7 +299,7 @@ struct Inflater {
     d++;
   }
   // len bytes from dist back (dist <= bytes of this member so far)
-  __device__ void copy(uint32_t dist, uint32_t len) {
+  __device__ __forceinline__ void copy(uint32_t dist, uint32_t len) {
     PQG_L uint8_t* ring = lds_ptr(sh->ring);
     __builtin_amdgcn_wave_barrier();
     uint32_t done = 0;
@@ -305,7 +318,7 @@ struct Inflater {
   }
 
   // ---- one DEFLATE stream (RFC 1951 3.2.3), kOK or kGZIP
-  __device__ int codes(const Huff& lc, const Huff& dc) {
+  __device__ __forceinline__ int codes(const Huff& lc, const Huff& dc) {
     for (;;) {
       const int sym = decode(lc);
       if (sym < 0) return kGZIP;
@@ -329,7 +342,7 @@ struct Inflater {
       maybe_flush();
     }
   }
-  __device__ int stored() {
+  __device__ __forceinline__ int stored() {
     align_byte();
     uint32_t a, b, c, e;
     if (!bits(8, &a) || !bits(8, &b) || !bits(8, &c) || !bits(8, &e)) return kGZIP;
@@ -344,7 +357,7 @@ struct Inflater {
     maybe_flush();
     return kOK;
   }
-  __device__ int fixed() {
+  __device__ __forceinline__ int fixed() {
     PQG_L uint16_t* L = lds_ptr(sh->lens);
     for (int s = lane; s < 288 + 30; s += 64)
       L[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
@@ -353,7 +366,7 @@ struct Inflater {
     build(sh->dist, sh->lens + 288, 30);
     return codes(sh->lit, sh->dist);
   }
-  __device__ int dynamic() {
+  __device__ __forceinline__ int dynamic() {
     uint32_t nlen, ndist, ncode;
     if (!bits(5, &nlen) || !bits(5, &ndist) || !bits(4, &ncode)) return kGZIP;
     nlen += 257;
@@ -428,7 +441,7 @@ struct Inflater {
       return kGZIP;
     return codes(sh->lit, sh->dist);
   }
-  __device__ int deflate() {
+  __device__ __forceinline__ int deflate() {
     uint32_t last, type;
     do {
       if (!bits(1, &last) || !bits(2, &type)) return kGZIP;
@@ -443,7 +456,7 @@ struct Inflater {
   }
 
   // ---- RFC 1952 members until the block ends (Go's multistream reader)
-  __device__ int run() {
+  __device__ __forceinline__ int run() {
     PQG_L uint32_t* T = lds_ptr(sh->crc_tab);
     for (int i = lane; i < 256; i += 64) {
       uint32_t c = (uint32_t)i;
