@@ -185,7 +185,8 @@ struct JobDev {
   const uint8_t* dict_data;  // dictionary entries (fixed width) or chars (var)
   int64_t dict_count, dict_len;
   const int64_t* dict_offs;  // variable-length dictionary: record start of each entry (count+1)
-  int32_t flags, pad;        // flags: bit0 INT96 nil entry (Q8), bit1 variable-length dictionary to walk
+  int32_t flags;             // bit0 INT96 nil entry (Q8), bit1 variable-length dictionary to walk
+  int32_t no_prewalk;        // host: the chunk is known not to be taken by the K1 prewalk / stride walk
   int64_t doffs_cap, doffs_base;  // dictionary-offsets arena region (entries)
   int64_t need_doffs;             // entries the dictionary needs (count+1)
   // ---- K1 speculative page scan (see k_page_cands / k_page_chain)

@@ -39,7 +39,7 @@ __global__ void k_cand_link(JobDev* jobs, const int* tile_job, int64_t total_til
                             int* ok2slot);
 __global__ void k_page_chain(JobDev* jobs, PageDev* pages, const Cand* cands, const int* succ,
                              const int* idx2slot, const int* ok2slot, int* order);
-__global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs, int prewalk);
+__global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs, int prewalk, int stride);
 __global__ void k_page_list(JobDev* jobs, PageDev* pages, int n_jobs, int* list, int list_cap, int* total,
                             int* queues);
 __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
@@ -188,6 +188,7 @@ struct pqg_ctx {
   bool dict4 = true;     // k_dict4 for 4-byte dictionary pages (PQG_DICT4=0: k_values<1>, for A/B runs)
   // Measured alternatives, off by default (C2 on one MI355X, r05_s8: run tables
   // 3.15 ms/step, in-kernel walk 3.33, fused 3.86):
+  bool stride = true;     // the K1 stride walk of equal-page chunks (PQG_STRIDE=0: the candidate scan takes them)
   bool dict_big = true;   // k_dict4_big for dictionaries past 4096 entries (PQG_DICT_BIG=0: k_dict4 gathers them)
   bool dict_walk = false; // PQG_DICT_WALK=1: k_dict_walk / k_dict_walk_g walk small pages' index streams themselves
   bool fused = false;     // PQG_FUSED=1: k_page_fused, levels + small 4-byte dictionary pages in one pass
@@ -213,7 +214,7 @@ struct pqg_ctx {
   std::vector<JobDev> plan;             // per-job capacities used
   std::vector<Caps> force;              // per-job capacities forced for this batch
   std::map<JobKey, Caps> learned;       // grown capacities, across calls
-  // chunks seen with more pages than the K1 prewalk takes: a batch of only
+  // chunks the K1 prewalk / stride walk did not take (scan_fallback != 2): a batch of only
   // such chunks skips the prewalk launch (performance only: the candidate
   // scan settles any chunk, so a stale entry never changes a result)
   std::map<JobKey, bool> many_pages;
@@ -280,6 +281,7 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
   if (const char* e = getenv("PQG_DICT4")) c->dict4 = atoi(e) != 0;
   if (const char* e = getenv("PQG_DICT_WALK")) c->dict_walk = atoi(e) != 0;
   if (const char* e = getenv("PQG_DICT_BIG")) c->dict_big = atoi(e) != 0;
+  if (const char* e = getenv("PQG_STRIDE")) c->stride = atoi(e) != 0;
   if (const char* e = getenv("PQG_FUSED")) c->fused = atoi(e) != 0;
   {
     hipFuncAttributes fa;
@@ -386,6 +388,7 @@ static int plan_batch(pqg_ctx* c) {
     d.codec = in.col.codec;
     d.has_dict_off = in.has_dict_page_offset;
     d.value_width = value_width_of(in.col);
+    d.no_prewalk = c->many_pages.count(JobKey{(uintptr_t)in.data, in.total_compressed_size, in.num_values_hint}) ? 1 : 0;
     int64_t pcap = in.total_compressed_size / 256 + 16;
     if (f.pages > 0) pcap = f.pages;
     pcap = std::min<int64_t>(pcap, (int64_t)1 << 30);
@@ -546,7 +549,7 @@ static int launch_pipeline(pqg_ctx* c) {
   int* tokoff = (int*)c->tile_okoff.p;
   // chunks of a few big pages (parquet-go's writer layout) are walked first
   // and skipped by the candidate scan
-  if (c->prewalk) hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n, kPrewalkPages);
+  if (c->prewalk) hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n, kPrewalkPages, (int)c->stride);
   if (nt > 0) {
     int64_t* cpos = (int64_t*)c->cand_pos.p;
     int* clist = (int*)c->cand_list.p;
@@ -565,7 +568,7 @@ static int launch_pipeline(pqg_ctx* c) {
                        tcount, toff, tokoff, cands, (int*)c->succ.p, (int*)c->idx2slot.p, (int*)c->ok2slot.p);
   hipLaunchKernelGGL(k_page_chain, dim3(n), dim3(1024), 0, s, jobs, pages, cands, (const int*)c->succ.p,
                      (const int*)c->idx2slot.p, (const int*)c->ok2slot.p, (int*)c->order.p);
-  hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n, 0);
+  hipLaunchKernelGGL(k_scan_pages, dim3(n), dim3(64), 0, s, jobs, pages, n, 0, 0);
   if (c->timed) hipEventRecord(c->ev[1], s);
   hipLaunchKernelGGL(k_page_list, dim3(n), dim3(1024), 0, s, jobs, pages, n, list,
                      (int)std::min<int64_t>(c->list_cap, INT32_MAX), ctr, ctr + 8);
@@ -770,7 +773,7 @@ int pqg_sync(pqg_ctx* c, pqg_chunk_result* results, int n_jobs) {
   }
   for (int i = 0; i < n; i++) {
     const JobDev& d = c->h_jobs[i];
-    if (d.status != PQG_ERR_CAPACITY && d.num_pages > kPrewalkPages) {
+    if (d.status != PQG_ERR_CAPACITY && d.scan_fallback != 2) {  // neither walked nor stride-walked by the prewalk
       if (c->many_pages.size() >= 65536) c->many_pages.clear();  // bounded: a cache, not a record
       const pqg_chunk_job& in = c->cur[(size_t)i];
       c->many_pages[JobKey{(uintptr_t)in.data, in.total_compressed_size, in.num_values_hint}] = true;

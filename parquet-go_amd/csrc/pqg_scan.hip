@@ -686,7 +686,139 @@ struct ScanShared {
   uint8_t win[kWin];
   SkipFrame frames[kMaxFrames];
   int16_t last[kMaxLast];
+  // the stride walk's per-lane candidate parses (parse_candidate)
+  __attribute__((aligned(16))) uint8_t cw[64][16 * kCandWin];
+  SkipFrame cf[64][kCandFrames];
+  int16_t cl[64][kCandLast];
 };
+
+// Chunks of equal small pages (fixed-width PLAIN columns: parquet-go's writer
+// cuts pages by row count, so every page but the last has one length and the
+// same header bytes): after the serial prewalk reached the first small data
+// page at `spos` with length `slen`, that page's header is parsed
+// (parse_candidate) and every later predicted page spos + k * slen is checked
+// against it byte for byte, 64 pages per round, one per lane, with one round
+// of loads: identical header bytes read identically (the same fields, shifted
+// positions), so the page's record is page 0's with its offsets.  The chunk's
+// last page (fewer rows) is parsed and must end at or past the chunk's end.
+// Any other difference returns false: the candidate scan then settles the
+// chunk and overwrites every page record written here.  The pages before
+// spos (a dictionary page, big pages) are the serial walk's.
+__device__ bool stride_walk(JobDev& job, int j, PageDev* pages, int64_t spos, int64_t slen, int np0, int64_t slots0,
+                            int64_t scratch0, ScanShared& sh) {
+  const int lane = lane_id();
+  const int64_t tcs = job.tcs;
+  if (slen <= 0 || tcs - spos <= 0) return false;
+  // page 0 of the stride (every lane parses it: wave-uniform result)
+  Cand c0;
+  parse_candidate(job, spos, sh.cf[lane], sh.cl[lane], lds_ptr(sh.cw[lane]), &c0);
+  const int64_t hl = c0.payload - spos;  // header bytes
+  if (c0.status != kOK || !(c0.type == 0 || c0.type == 3) || c0.next - spos != slen || hl <= 0 || hl > 64)
+    return false;
+  // page 0's header bytes: LDS bytes [0, hl) of sh.win (16 granules max)
+  const gcu8 base = gconst(job.data);
+  constexpr int kHG = 5;  // granules holding a <= 64-byte header from any alignment
+  {
+    const uintptr_t a0 = (uintptr_t)(base + spos) & ~(uintptr_t)15;
+    const int64_t at = (int64_t)(a0 + 16 * (uintptr_t)lane - (uintptr_t)base);
+    const uint4 g = ldg16(lane < kHG && at < job.data_len ? a0 + 16 * lane : a0);  // granules holding a chunk byte
+    if (lane < kHG) sts16(lds_ptr(sh.win) + 16 * lane, g);
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t off0 = (uint32_t)((uintptr_t)(base + spos) & 15);
+  const int64_t npages = (tcs - spos + slen - 1) / slen;
+  int64_t slots = slots0, scratch = scratch0;
+  const int64_t nv0 = c0.num_values, cp0 = c0.comp;
+  for (int64_t k0 = 0; k0 < npages; k0 += 64) {
+    const int64_t k = k0 + lane;
+    const bool live = k < npages;
+    const int64_t q = spos + (live ? k : 0) * slen;
+    // this lane's page header bytes: kHG granules from q's aligned address
+    const uintptr_t a = (uintptr_t)(base + q) & ~(uintptr_t)15;
+    uint4 g[kHG];
+#pragma unroll
+    for (int t = 0; t < kHG; t++) {
+      const int64_t at = (int64_t)(a + 16 * t - (uintptr_t)base);
+      g[t] = ldg16(at < job.data_len ? a + 16 * t : a);
+    }
+    PQG_L uint32_t* W = (PQG_L uint32_t*)lds_ptr(sh.cw[lane]);
+#pragma unroll
+    for (int t = 0; t < kHG; t++) sts16((PQG_L uint8_t*)W + 16 * t, g[t]);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t offk = (uint32_t)((uintptr_t)(base + q) & 15);
+    const PQG_L uint32_t* W0 = (const PQG_L uint32_t*)lds_ptr(sh.win);
+    bool same = live;
+    for (int i = 0; i < (int)hl; i += 4) {
+      const uint32_t ok_ = offk + (uint32_t)i, o0 = off0 + (uint32_t)i;
+      const uint32_t x = __builtin_amdgcn_alignbit(W[(ok_ >> 2) + 1], W[ok_ >> 2], (ok_ & 3) * 8);
+      const uint32_t y = __builtin_amdgcn_alignbit(W0[(o0 >> 2) + 1], W0[o0 >> 2], (o0 & 3) * 8);
+      const int r = (int)hl - i;
+      const uint32_t m = r >= 4 ? 0xffffffffu : ((1u << (8 * r)) - 1);
+      same &= ((x ^ y) & m) == 0;
+    }
+    // the header past the chunk's end cannot be page 0's
+    same &= q + hl <= tcs;
+    __builtin_amdgcn_wave_barrier();
+    const bool lastp = live && k == npages - 1;
+    Cand ck = c0;
+    bool ok = same;
+    if (live && !same) {
+      if (lastp) {  // the short last page: parsed, and it must end the chunk
+        parse_candidate(job, q, sh.cf[lane], sh.cl[lane], lds_ptr(sh.cw[lane]), &ck);
+        ok = ck.status == kOK && (ck.type == 0 || ck.type == 3) && ck.next >= tcs;
+      }
+    } else if (same) {  // page 0's fields at this page's position
+      ck.pos = q;
+      ck.payload = c0.payload + (q - spos);
+      ck.next = c0.next + (q - spos);
+      // classify_page's size check at this position (an understated buffer),
+      // and a full-length last page ends the chunk exactly
+      ok = ck.next <= job.data_len && (!lastp || ck.next >= tcs);
+    }
+    const uint64_t lb = __ballot(live), okb = __ballot(live && ok);
+    if (okb != lb) return false;
+    const int nl = __popcll(lb);
+    const bool mine = live;
+    const int64_t nv = mine ? ck.num_values : 0, cp = mine ? ck.comp : 0;
+    const int64_t inv = (int64_t)wave_incl_scan_u64((uint64_t)nv), icp = (int64_t)wave_incl_scan_u64((uint64_t)cp);
+    if (mine && np0 + k < job.page_cap) {
+      PageDev pg;
+      init_page(pg, j, q, ck.payload);
+      pg.page_type = ck.type;
+      pg.encoding = ck.encoding;
+      pg.num_values = ck.num_values;
+      pg.csize = ck.csize;
+      pg.usize = ck.usize;
+      pg.def_len = ck.def_len;
+      pg.rep_len = ck.rep_len;
+      pg.def_enc = ck.def_enc;
+      pg.rep_enc = ck.rep_enc;
+      pg.read_status = kOK;
+      pg.slot_offset = slots + inv - nv;
+      if (cp > 0) pg.scratch_offset = scratch + icp - cp;
+      pages[job.page_base + np0 + k] = pg;
+    }
+    auto lane64 = [](int64_t v, int l) {
+      return (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l) << 32);
+    };
+    slots += lane64(inv, nl - 1);
+    scratch += lane64(icp, nl - 1);
+  }
+  (void)nv0;
+  (void)cp0;
+  if (lane == 0) {
+    const int np = np0 + (int)npages;
+    init_job_results(job);
+    job.scan_fallback = 2;
+    job.num_pages = np;
+    job.scan_status = kOK;
+    job.need_scratch = scratch;
+    job.num_slots = slots;
+    if (np > job.page_cap || slots > job.slot_cap || scratch > job.scratch_cap) job.status = kCAPACITY;
+  }
+  return true;
+}
 
 // prewalk > 0: before the candidate scan, chunks of at most `prewalk` big
 // pages (each data page >= 1/8 of the chunk: parquet-go's writer puts a whole
@@ -695,17 +827,19 @@ struct ScanShared {
 // decides; only a walk that reaches the chunk's end (or its first failing
 // page) within the limit is redone with its page records.  prewalk == 0: the
 // jobs the speculative path could not settle (scan_fallback == 1).
-__global__ void __launch_bounds__(64) k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs, int prewalk) {
+__global__ void __launch_bounds__(64) k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs, int prewalk, int stride) {
   __shared__ __attribute__((aligned(16))) ScanShared sh;
   int j = blockIdx.x;
   if (j >= n_jobs) return;
   JobDev& job = jobs[j];
   const int64_t tcs = job.tcs;
   if (prewalk > 0) {
-    if (job.scan_fallback || tcs <= 0) return;
+    if (job.scan_fallback || tcs <= 0 || job.no_prewalk) return;
     Window win{gconst(job.data), job.data_len, kFarAway, lds_ptr(sh.win)};
     int64_t pos = 0;
     bool dict_seen = false, done = false;
+    int64_t spos = -1, slen = 0;  // the first small data page (a stride walk's start)
+    int snp = 0;
     for (int np = 0;; np++) {
       if (tcs - pos <= 0) {
         done = true;
@@ -732,11 +866,56 @@ __global__ void __launch_bounds__(64) k_scan_pages(JobDev* jobs, PageDev* pages,
         done = true;
         break;
       }
-      if (h.type != 2 && next - pos < tcs / 8) break;  // small pages: many of them, the candidate scan
+      if (h.type != 2 && next - pos < tcs / 8) {  // small pages: many of them, a stride walk or the candidate scan
+        spos = pos;
+        slen = next - pos;
+        snp = np;
+        break;
+      }
       if (h.type == 2) dict_seen = true;
       pos = next;
     }
-    if (!done) return;
+    if (!done) {
+      if (spos < 0 || !stride) return;
+      // the pages before spos (serially, with their records), then the stride
+      Window w2{gconst(job.data), job.data_len, kFarAway, lds_ptr(sh.win)};
+      int64_t p2 = 0, slots = 0, scratch = 0;
+      int dict_page = -1;
+      bool ds2 = false;
+      for (int k = 0; k < snp; k++) {
+        Compact<WinSrc> c;
+        c.src.w = w2;
+        c.pos = p2;
+        c.frames = sh.frames;
+        c.last = sh.last;
+        c.nlast = 0;
+        c.last_id = 0;
+        c.bool_set = false;
+        c.bool_val = false;
+        PageHdr h;
+        int e = c.read_page_header(&h);
+        w2 = c.src.w;
+        PageDev pg;
+        init_page(pg, j, p2, c.pos);
+        pg.slot_offset = slots;
+        int64_t next, comp;
+        e = classify_page(job, h, e, c.pos, ds2, pg, &next, &comp);
+        if (comp > 0) {
+          pg.scratch_offset = scratch;
+          scratch += comp;
+        }
+        pg.read_status = e;
+        if (k < job.page_cap && lane_id() == 0) pages[job.page_base + k] = pg;
+        if (h.type == 0 || h.type == 3) slots += pg.num_values;
+        if (h.type == 2) {
+          ds2 = true;
+          dict_page = k;
+        }
+        p2 = next;
+      }
+      if (stride_walk(job, j, pages, spos, slen, snp, slots, scratch, sh) && lane_id() == 0) job.dict_page = dict_page;
+      return;
+    }
   } else if (job.scan_fallback != 1) {
     return;
   }

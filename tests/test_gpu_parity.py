@@ -29,6 +29,26 @@ def dec():
     d.close()
 
 
+@pytest.fixture(scope="module")
+def dec_scan():
+    """A decoder without the K1 stride walk (PQG_STRIDE=0, read at context
+    creation): chunks of equal pages then take the candidate scan, which the
+    scan tests below exercise."""
+    import os
+    import pqgpu
+    old = os.environ.get("PQG_STRIDE")
+    os.environ["PQG_STRIDE"] = "0"
+    try:
+        d = pqgpu.GpuDecoder(0)
+    finally:
+        if old is None:
+            os.environ.pop("PQG_STRIDE", None)
+        else:
+            os.environ["PQG_STRIDE"] = old
+    yield d
+    d.close()
+
+
 def test_c1_plain_int64(dec):
     data, _ = W.config_c1(rows=200_000, rows_per_page=20000)
     P.compare_file(data, dec)
@@ -349,18 +369,18 @@ def test_scan_big_pages_prewalked(dec):
     P.compare_file(bytes(b), dec)
 
 
-def test_scan_false_candidates_are_skipped(dec):
+def test_scan_false_candidates_are_skipped(dec_scan):
     # PLAIN int32 payload bytes 15 00 15 00 parse as page-header prefixes: a few
     # per tile are false candidates the chain must jump over
     n = 60_000
     v = np.arange(n, dtype=np.int32)
     v[::997] = 0x00150015
     data = W.write_file([W.Column("x", W.INT32, v, rows_per_page=5000)], n)
-    walk, cands, pages, _ = _decode_one(dec, data)
+    walk, cands, pages, _ = _decode_one(dec_scan, data)
     assert walk == 0 and pages == 12 and cands > pages
 
 
-def test_scan_false_ok_headers_walked(dec):
+def test_scan_false_ok_headers_walked(dec_scan):
     # a complete, valid DataPageHeader embedded in PLAIN payload bytes: an ok
     # false candidate between two real pages (the chain is walked around it)
     fake = bytes([0x15, 0x00, 0x15, 0x02, 0x15, 0x02, 0x2C, 0x15, 0x02, 0x15, 0x00, 0x15, 0x00, 0x15, 0x00,
@@ -372,27 +392,70 @@ def test_scan_false_ok_headers_walked(dec):
         v[at:at + len(fk)] = fk
     for codec in (W.UNCOMPRESSED, W.SNAPPY):
         data = W.write_file([W.Column("x", W.INT32, v, rows_per_page=5000, codec=codec)], n)
-        walk, cands, pages, _ = _decode_one(dec, data)
+        walk, cands, pages, _ = _decode_one(dec_scan, data)
         assert walk == 0 and pages == 12
 
 
-def test_scan_tile_overflow_falls_back(dec):
+def test_scan_stride_walk(dec):
+    # equal pages (fixed-width PLAIN, rows per page fixed): the prewalk checks
+    # the predicted page positions 64 at a time and the candidate scan is skipped
+    n = 200_003
+    v = np.arange(n, dtype=np.int64) * 7
+    data = W.write_file([W.Column("x", W.INT64, v, rows_per_page=1000)], n)  # 201 pages, the last short
+    walk, cands, pages, _ = _decode_one(dec, data)
+    assert walk == 2 and cands == 0 and pages == 201
+    # a dictionary page first, then equal data pages (the serial part, then the stride)
+    data = W.config_c4(rows=30_000, vocab=500, rows_per_page=1000, codec=W.UNCOMPRESSED)[0]
+    P.compare_file(data, dec)
+    # optional columns: equal pages only when the null pattern is regular
+    d = (np.arange(n) % 3 != 0).astype(np.uint8)
+    vv = v[d.astype(bool)]
+    data = W.write_file([W.Column("x", W.INT64, vv, repetition=W.OPTIONAL, def_levels=d, rows_per_page=999)], n)
+    P.compare_file(data, dec)
+
+
+def test_scan_stride_walk_mispredicted(dec):
+    # damaged headers at predicted page positions, a page of another length,
+    # bytes past the last page: the stride walk gives up (or reads the same
+    # error) and the result is the oracle's
+    import pqgpu
+    n = 60_000
+    v = np.arange(n, dtype=np.int32)
+    data = W.write_file([W.Column("x", W.INT32, v, rows_per_page=5000)], n)
+    m = pqgpu.ParquetFile(data).chunk_meta(0, 0)
+    L = data.index(b"\x15\x00\x15", m.start + 3) - m.start  # the first page's length
+    rng = np.random.default_rng(41)
+    for _ in range(16):
+        b = bytearray(data)
+        k = int(rng.integers(1, n // 5000))
+        b[m.start + k * L + int(rng.integers(0, 12))] ^= int(rng.integers(1, 256))
+        P.compare_file(bytes(b), dec)
+    # one page of another length in the middle
+    v2 = np.concatenate([v[:20000], v[:1], v[20000:]])
+    cols = [W.Column("x", W.INT32, v2, rows_per_page=5000)]
+    P.compare_file(W.write_file(cols, n + 1), dec)
+
+
+def test_scan_tile_overflow_falls_back(dec_scan):
     # every value is a header prefix: > kCandPerTile hits per tile -> serial walk
     n = 40_000
     v = np.full(n, 0x00150015, dtype=np.int32)
     data = W.write_file([W.Column("x", W.INT32, v, rows_per_page=9000)], n)
-    walk, _, pages, _ = _decode_one(dec, data)
+    walk, _, pages, _ = _decode_one(dec_scan, data)
     assert walk == 1 and pages == 5
 
 
-def test_scan_tiny_pages(dec):
-    # many pages per 16 KiB tile (fallback or not, the page list must match)
+def test_scan_tiny_pages(dec, dec_scan):
+    # many pages per 16 KiB tile (fallback or not, the page list must match);
+    # with the stride walk too (715 equal pages of ~90 bytes)
     n = 5000
     v = np.arange(n, dtype=np.int64)
     data = W.write_file([W.Column("x", W.INT64, v, rows_per_page=7)], n)
-    P.compare_file(data, dec)
-    data = W.write_file([W.Column("x", W.INT64, v, rows_per_page=300)], n)
+    P.compare_file(data, dec_scan)
     walk, _, pages, _ = _decode_one(dec, data)
+    assert walk == 2 and pages == (n + 6) // 7
+    data = W.write_file([W.Column("x", W.INT64, v, rows_per_page=300)], n)
+    walk, _, pages, _ = _decode_one(dec_scan, data)
     assert walk == 0 and pages == (n + 299) // 300
 
 
