@@ -104,10 +104,13 @@ enum {
 enum {
   PQG_PAGE_FLAG_INT96_NIL = 1,  /* Q8: truncated final INT96 value left nil by the
                                    reference (type_int96.go:21-42); bytes are 0 */
-  PQG_PAGE_FLAG_SNAPPY_SERIAL = 2 /* libpqgpu diagnostic: the page's snappy block was
+  PQG_PAGE_FLAG_SNAPPY_SERIAL = 2, /* libpqgpu diagnostic: the page's snappy block was
                                    decoded whole by one wave (its 64 KiB sub-block
                                    split failed: a copy across a 64 KiB block
                                    boundary, or a corrupt block) */
+  PQG_PAGE_FLAG_FUSED = 32        /* libpqgpu diagnostic: the page's levels and
+                                   dictionary keys were decoded in one pass
+                                   (k_page_fused, PQG_FUSED=1; off by default) */
 };
 
 /* ---- column / chunk description ----------------------------------------- */
