@@ -298,7 +298,8 @@ constexpr int kQueueDictWalk = 15;   // small 4-byte dictionary pages walked in-
 constexpr int kQueueDictWalkG = 16;  // the same, dictionary gathered from global memory (k_dict_walk_g)
 constexpr int kQueueLevGen = 17;  // k_page_levels when k_page_levels_w1 takes the w = 1 jobs' pages
 constexpr int kQueueDictBig = 18; // k_dict4_big: run-table pages of dictionaries past 4096 entries
-constexpr int kQueueSlots = 19;
+constexpr int kQueueWalkWave = 19;  // k_walk_wave: one wave per value stream
+constexpr int kQueueSlots = 20;
 constexpr int kPresentBigDict = 8;  // stage flag (kModePresentOff + 8): a page for k_dict4_big  // queue regions zeroed per launch: 0-8, the stage flags (9), 10-16
 
 // Scan tiles of the speculative page-header search.

@@ -39,6 +39,8 @@ __global__ void k_cand_link(JobDev* jobs, const int* tile_job, int64_t total_til
                             int* ok2slot);
 __global__ void k_page_chain(JobDev* jobs, PageDev* pages, const Cand* cands, const int* succ,
                              const int* idx2slot, const int* ok2slot, int* order);
+__global__ void k_walk_wave(const PageDev* pages, const int* list, const int* total, int* queue, HStream* streams,
+                            RunEnt* runs, BlockDesc* blks, int skip_dict_small);
 __global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs, int prewalk, int stride);
 __global__ void k_page_list(JobDev* jobs, PageDev* pages, int n_jobs, int* list, int list_cap, int* total,
                             int* queues);
@@ -188,6 +190,7 @@ struct pqg_ctx {
   bool dict4 = true;     // k_dict4 for 4-byte dictionary pages (PQG_DICT4=0: k_values<1>, for A/B runs)
   // Measured alternatives, off by default (C2 on one MI355X, r05_s8: run tables
   // 3.15 ms/step, in-kernel walk 3.33, fused 3.86):
+  bool walk_wave = false; // PQG_WALK_WAVE=1: k_walk_wave (one wave per value stream) for the run tables
   bool stride = true;     // the K1 stride walk of equal-page chunks (PQG_STRIDE=0: the candidate scan takes them)
   bool dict_big = true;   // k_dict4_big for dictionaries past 4096 entries (PQG_DICT_BIG=0: k_dict4 gathers them)
   bool dict_walk = false; // PQG_DICT_WALK=1: k_dict_walk / k_dict_walk_g walk small pages' index streams themselves
@@ -282,6 +285,7 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
   if (const char* e = getenv("PQG_DICT_WALK")) c->dict_walk = atoi(e) != 0;
   if (const char* e = getenv("PQG_DICT_BIG")) c->dict_big = atoi(e) != 0;
   if (const char* e = getenv("PQG_STRIDE")) c->stride = atoi(e) != 0;
+  if (const char* e = getenv("PQG_WALK_WAVE")) c->walk_wave = atoi(e) != 0;
   if (const char* e = getenv("PQG_FUSED")) c->fused = atoi(e) != 0;
   {
     hipFuncAttributes fa;
@@ -632,9 +636,14 @@ static int launch_pipeline(pqg_ctx* c) {
   LongWalk* wlong = (LongWalk*)c->walk_long.p;
   const int wlc = (int)std::min<int64_t>(c->walk_long_cap, INT32_MAX);
   const int walk_small = c->dict4 && c->dict_walk;  // small 4-byte dictionary pages: walked in k_dict4
-  hipLaunchKernelGGL(k_hybrid_walk, dim3(walk_blocks), dim3(kWalkLanes), 0, s, pages, list, ctr, streams, runs, blks,
-                     wlong, wlc, walk_small);
-  hipLaunchKernelGGL(k_walk_long, dim3(c->num_cus * 2), dim3(256), 0, s, ctr, wlong, wlc, blks);
+  if (c->walk_wave) {  // one wave per value stream (pqg_tablewalk.hip)
+    hipLaunchKernelGGL(k_walk_wave, dim3(qgrid(c->num_cus * 20)), dim3(64), 0, s, pages, list, ctr, Q(kQueueWalkWave),
+                       streams, runs, blks, walk_small);
+  } else {  // one lane per value stream
+    hipLaunchKernelGGL(k_hybrid_walk, dim3(walk_blocks), dim3(kWalkLanes), 0, s, pages, list, ctr, streams, runs, blks,
+                       wlong, wlc, walk_small);
+    hipLaunchKernelGGL(k_walk_long, dim3(c->num_cus * 2), dim3(256), 0, s, ctr, wlong, wlc, blks);
+  }
   if (c->timed) hipEventRecord(c->ev[5], s);
   if (c->timed) hipEventRecord(c->ev[6], s);
   PartRec* parts = (PartRec*)c->parts.p;

@@ -984,7 +984,7 @@ __global__ void __launch_bounds__(64) k_scan_pages(JobDev* jobs, PageDev* pages,
 // stream's run table / block index — an exclusive scan of a bound from the
 // page's sizes (the same bound reg_stream used to take with two contended
 // atomics per page): a value stream of B bytes and n values has at most
-// B/2 + 2 runs and n/kHBlock + runs/kHBlockRuns + B/(kHBlockBytes/2) + 3 blocks.
+// B/2 + 2 runs and 2 n/kHBlock + 2 runs/kHBlockRuns + B/(kHBlockBytes/2) + 5 blocks.
 __global__ void __launch_bounds__(1024) k_page_list(JobDev* jobs, PageDev* pages, int n_jobs, int* list, int list_cap,
                                                     int* total, int* queues) {
   __shared__ int64_t part[17];
@@ -1031,7 +1031,10 @@ __global__ void __launch_bounds__(1024) k_page_list(JobDev* jobs, PageDev* pages
     if (i < n && (cur.type == 0 || cur.type == 3)) {
       const int64_t B = cur.so >= 0 ? (int64_t)(uint32_t)cur.usize : (int64_t)(uint32_t)cur.csize;
       nr = B / 2 + 2;
-      nb = (int64_t)(uint32_t)cur.nv / kHBlock + nr / kHBlockRuns + B / (kHBlockBytes / 2) + 3;
+      // the lane walker's greedy blocks need n/kHBlock + runs/kHBlockRuns +
+      // B/(kHBlockBytes/2) + 3; the wave walker's merged batches up to twice
+      // the first two terms (pqg_tablewalk.hip)
+      nb = 2 * (int64_t)(uint32_t)cur.nv / kHBlock + 2 * nr / kHBlockRuns + B / (kHBlockBytes / 2) + 5;
     }
     int64_t tr, tb;
     const int64_t er = block_excl_scan<1024>(nr, &tr, part);

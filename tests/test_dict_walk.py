@@ -73,10 +73,12 @@ def dict_chunk(rng, pages, w, dcount, nullable=True, bad_frac=0.0, short_frac=0.
     return b"".join(parts)
 
 
-# the three decode paths of 4-byte dictionary pages (pqg_runtime.hip): run
-# tables + k_dict4 (default), the in-kernel walk (PQG_DICT_WALK=1) and the
-# fused level + index pass (PQG_FUSED=1); read when the context is created
-PATHS = {"tables": {}, "walk": {"PQG_DICT_WALK": "1"}, "fused": {"PQG_DICT_WALK": "1", "PQG_FUSED": "1"}}
+# the decode paths of 4-byte dictionary pages (pqg_runtime.hip): run tables
+# from the lane walker + k_dict4 (default), run tables from the wave walker
+# (PQG_WALK_WAVE=1), the in-kernel walk (PQG_DICT_WALK=1) and the fused level
+# + index pass (PQG_FUSED=1); read when the context is created
+PATHS = {"tables": {}, "wave_tables": {"PQG_WALK_WAVE": "1"}, "walk": {"PQG_DICT_WALK": "1"},
+         "fused": {"PQG_DICT_WALK": "1", "PQG_FUSED": "1"}}
 
 
 @pytest.fixture(scope="module", params=list(PATHS))
@@ -84,7 +86,7 @@ def dec(request):
     import os
     import pqgpu
     env = PATHS[request.param]
-    old = {k: os.environ.get(k) for k in ("PQG_DICT_WALK", "PQG_FUSED")}
+    old = {k: os.environ.get(k) for k in ("PQG_DICT_WALK", "PQG_FUSED", "PQG_WALK_WAVE")}
     os.environ.update(env)
     try:
         d = pqgpu.GpuDecoder(0)
