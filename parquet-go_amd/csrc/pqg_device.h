@@ -215,6 +215,11 @@ __device__ __forceinline__ void store_run_aligned(uintptr_t base, const uint32_t
       if (NT) {
         const u32x4_t v = {w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]};
         __builtin_nontemporal_store(v, (PQG_G u32x4_t*)(o + 16 * g));
+      } else if (D >= 8) {
+        // each instruction writes every other granule of the wave's span:
+        // write-back stores, so the L2 merges the halves of each line (the
+        // non-temporal ones went out as half lines, see store_run64)
+        stg16(o + 16 * g, make_uint4(w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]));
       } else {
         stg16o(o + 16 * g, make_uint4(w[4 * g], w[4 * g + 1], w[4 * g + 2], w[4 * g + 3]));
       }
