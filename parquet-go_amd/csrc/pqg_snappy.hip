@@ -839,20 +839,24 @@ struct SnapBlock {
 #pragma unroll
       for (int k = 0; k < 16; k++) chase |= own[k] >= pre && own[k] < kSpan;
       if (__ballot(chase)) {
+        // byte x's source at S[(x % 16) * 64 + x / 16]: lane L's byte k at
+        // k * 64 + L, so each store instruction writes 64 consecutive dwords,
+        // and a gather of a nearby byte (copy offsets are mostly short) by
+        // consecutive lanes reads consecutive dwords: no bank conflicts
+        // (byte-major, lane stride 16 dwords, every gather of the doubling
+        // was a 16-way conflict)
         PQG_L int32_t* S = lds_ptr(sh->src);
         for (int r = 0; r < 11; r++) {
 #pragma unroll
-          for (int k = 0; k < 4; k++)
-            *(PQG_L u32x4_t*)(S + 16 * lane + 4 * k) =
-                u32x4_t{(uint32_t)own[4 * k], (uint32_t)own[4 * k + 1], (uint32_t)own[4 * k + 2],
-                        (uint32_t)own[4 * k + 3]};
+          for (int k = 0; k < 16; k++) S[64 * k + lane] = own[k];
           __builtin_amdgcn_wave_barrier();
           chase = false;
 #pragma unroll
           for (int k = 0; k < 16; k++) {
             // unconditional loads (a guarded load would wait on its own)
             const bool in = own[k] >= pre && own[k] < kSpan;
-            const int32_t nv = S[in ? own[k] : 0];
+            const int32_t x = in ? own[k] : 0;
+            const int32_t nv = S[((x & 15) << 6) | (x >> 4)];
             own[k] = in ? nv : own[k];
             chase |= own[k] >= pre && own[k] < kSpan;
           }
