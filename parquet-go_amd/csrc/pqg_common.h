@@ -278,6 +278,10 @@ struct LongWalk {
 #define PQG_WALK_THREADS 64
 #endif
 constexpr int kWalkThreads = PQG_WALK_THREADS;
+#ifndef PQG_PW_THREADS
+#define PQG_PW_THREADS 256
+#endif
+constexpr int kPwThreads = PQG_PW_THREADS;  // k_str_plain block size (PLAIN byte-array length walk)
 
 // Work queues: kQShards heads kQStride ints apart (see queue_pull, pqg_device.h).
 constexpr int kQShards = 8;

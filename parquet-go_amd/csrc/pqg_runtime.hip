@@ -685,7 +685,7 @@ static int launch_pipeline(pqg_ctx* c) {
   if (c->any_var) {
     int64_t* offs = (int64_t*)c->offs_arena.p;
     hipLaunchKernelGGL(k_str_dict, dim3(n), dim3(512), 0, s, jobs, pages, (int64_t*)c->doffs_arena.p);
-    hipLaunchKernelGGL(k_str_plain, dim3(qgrid(c->num_cus * 4)), dim3(512), 0, s, jobs, pages, list, ctr, Q(5), offs);
+    hipLaunchKernelGGL(k_str_plain, dim3(qgrid(c->num_cus * 4 * 512 / kPwThreads)), dim3(kPwThreads), 0, s, jobs, pages, list, ctr, Q(5), offs);
     hipLaunchKernelGGL(k_str_count, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, parts, ctr, Q(4), offs, streams,
                        runs, blks);
     hipLaunchKernelGGL(k_str_delta, dim3(qgrid(c->num_cus * 8)), dim3(64), 0, s, jobs, pages, list, ctr,

@@ -54,9 +54,9 @@ int prof_read_strings(unsigned long long* out) {
 // dictionary pages).
 //
 // The chain 0 -> 4 + len(0) -> ... is serial, but it is walked in parallel,
-// 32 KiB of the stream at a time: the chunk is staged in LDS with one round
+// 17 KiB of the stream at a time: the chunk is staged in LDS with one round
 // of coalesced loads (the next chunk's loads are in flight meanwhile), each of
-// the 512 threads takes a 64-byte segment, guesses where the chain enters it
+// the 256 threads takes a 68-byte segment, guesses where the chain enters it
 // (the first position whose length chain is valid for three records; the
 // segment holding the known chain position takes that) and walks its records
 // from there, keeping their ends in registers.  The guesses are then checked
@@ -69,19 +69,20 @@ int prof_read_strings(unsigned long long* out) {
 // whether the chunk takes the serial walk (for text-like records: never).
 // ---------------------------------------------------------------------------
 constexpr int kWalkT = 512;
+constexpr int kPwT = kPwThreads;            // block_walk / k_str_plain block size (pqg_common.h)
 constexpr int kPwSeg = 68;                  // bytes per thread segment (17 dwords: the lanes' reads
                                             // at the same offset of their segments hit distinct banks)
-constexpr int kPwChunk = kWalkT * kPwSeg;   // bytes per chunk (LDS)
+constexpr int kPwChunk = kPwT * kPwSeg;   // bytes per chunk (LDS)
 constexpr int kPwRec = kPwSeg / 4;          // records a segment can hold (>= 4 bytes each)
 constexpr int kPwAhead = 4096;              // staged past the chunk: the guesses' chain checks
 constexpr int kPwStage = kPwChunk + kPwAhead + 64;
-constexpr int kPwG = (kPwStage / 16 + kWalkT - 1) / kWalkT;  // staged granules per thread
+constexpr int kPwG = (kPwStage / 16 + kPwT - 1) / kPwT;  // staged granules per thread
 
 struct BlockWalkShared {
-  uint8_t buf[kPwG * kWalkT * 16];  // the chunk from its 16-aligned start, + kPwAhead + 64 bytes
-  uint32_t X[kWalkT];          // per segment: exit (chain position after its records)
-  int64_t part[kWalkT / 64 + 1];
-  int keys[kWalkT / 64];
+  uint8_t buf[kPwG * kPwT * 16];  // the chunk from its 16-aligned start, + kPwAhead + 64 bytes
+  uint32_t X[kPwT];          // per segment: exit (chain position after its records)
+  int64_t part[kPwT / 64 + 1];
+  int keys[kPwT / 64];
   uint32_t cur;                // the true chain position (the first record start not yet placed)
   uint32_t idx;                // records placed
   uint32_t last_end;           // end of record count - 1
@@ -119,7 +120,7 @@ __device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out
     const uintptr_t A = (uintptr_t)(p + c0) & ~(uintptr_t)15;
 #pragma unroll
     for (int k = 0; k < kPwG; k++) {
-      const uintptr_t g = A + 16 * (uintptr_t)(t + kWalkT * k);
+      const uintptr_t g = A + 16 * (uintptr_t)(t + kPwT * k);
       v[k] = ldg16(g < lastg ? g : lastg);
     }
   };
@@ -137,7 +138,7 @@ __device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out
     }
     // stage this chunk, then start the next one's loads
 #pragma unroll
-    for (int k = 0; k < kPwG; k++) sts16(lds_ptr(sh.buf) + 16 * (t + kWalkT * k), nx[k]);
+    for (int k = 0; k < kPwG; k++) sts16(lds_ptr(sh.buf) + 16 * (t + kPwT * k), nx[k]);
     __syncthreads();
     if (c1 < n) load_chunk(c1, nx);
     PQG_ACC0(21, 1);
@@ -260,7 +261,7 @@ __device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out
     const int any_bad = __syncthreads_or(bad);
     if (!any_bad) {
       int64_t tot;
-      const int64_t base = (int64_t)idx0 + block_excl_scan<kWalkT>(has ? (int64_t)k : 0, &tot, sh.part);
+      const int64_t base = (int64_t)idx0 + block_excl_scan<kPwT>(has ? (int64_t)k : 0, &tot, sh.part);
 #pragma unroll
       for (int j = 0; j < kPwRec; j++) {
         const int64_t i = base + j;
@@ -272,7 +273,7 @@ __device__ int block_walk(gcu8 p, uint32_t n, uint32_t count, PQG_G int64_t* out
       // the last segment with records hands the chain on (the exit of the chunk)
       const int last = __shfl(key, 63, 64);  // this wave's; the block's is the max over waves
       int blast = 0;
-      for (int w = 0; w < kWalkT / 64; w++) blast = sh.keys[w] > blast ? sh.keys[w] : blast;
+      for (int w = 0; w < kPwT / 64; w++) blast = sh.keys[w] > blast ? sh.keys[w] : blast;
       (void)last;
       if (t == 0) {
         sh.idx = idx0 + (uint32_t)(tot < (int64_t)(count - idx0) ? tot : (int64_t)(count - idx0));
@@ -553,7 +554,10 @@ __global__ void __launch_bounds__(kWalkT) k_str_dict(JobDev* jobs, PageDev* page
 }
 
 // ---- K7b (PLAIN) -------------------------------------------------------------
-__global__ void __launch_bounds__(kWalkT) k_str_plain(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+#ifndef PQG_PW_WPE
+#define PQG_PW_WPE 4
+#endif
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, kPwT), amdgpu_waves_per_eu(PQG_PW_WPE))) k_str_plain(JobDev* jobs, PageDev* pages, const int* list, const int* total,
                                                       int* queue, int64_t* offs_arena) {
   __shared__ BlockWalkShared sh;
   __shared__ int s_t;
