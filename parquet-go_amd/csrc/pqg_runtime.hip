@@ -195,6 +195,9 @@ struct pqg_ctx {
   bool dict_big = true;   // k_dict4_big for dictionaries past 4096 entries (PQG_DICT_BIG=0: k_dict4 gathers them)
   bool dict_walk = false; // PQG_DICT_WALK=1: k_dict_walk / k_dict_walk_g walk small pages' index streams themselves
   bool fused = false;     // PQG_FUSED=1: k_page_fused, levels + small 4-byte dictionary pages in one pass
+  int seg_waves = 31;     // PQG_SEG_WAVES: k_snap_seg waves per CU (its 5 KiB of LDS allow 31; 16: C4 +10 %)
+  int levlong_waves = 8;  // PQG_LEVLONG_WAVES: k_level_long waves per CU
+  int link_waves = 16;    // PQG_LINK_WAVES: k_snap_link waves per CU (one wave per big page; 4: C4 +50 %)
   DevBuf lookback;       // k_page_fused: one look-back word per page
   int snappy_per_cu = 2;  // resident k_snappy waves per CU (LDS-bound: the output history ring)
   DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
@@ -287,6 +290,9 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
   if (const char* e = getenv("PQG_STRIDE")) c->stride = atoi(e) != 0;
   if (const char* e = getenv("PQG_WALK_WAVE")) c->walk_wave = atoi(e) != 0;
   if (const char* e = getenv("PQG_FUSED")) c->fused = atoi(e) != 0;
+  if (const char* e = getenv("PQG_SEG_WAVES")) c->seg_waves = atoi(e) > 0 ? atoi(e) : c->seg_waves;
+  if (const char* e = getenv("PQG_LEVLONG_WAVES")) c->levlong_waves = atoi(e) > 0 ? atoi(e) : c->levlong_waves;
+  if (const char* e = getenv("PQG_LINK_WAVES")) c->link_waves = atoi(e) > 0 ? atoi(e) : c->link_waves;
   {
     hipFuncAttributes fa;
     if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_dict4)) == hipSuccess && fa.maxThreadsPerBlock > 0)
@@ -519,8 +525,8 @@ static void launch_snappy(pqg_ctx* c, hipStream_t s, JobDev* jobs, PageDev* page
   hipMemsetAsync(sctr, 0, 2 * sizeof(int), s);
   hipLaunchKernelGGL(k_snap_plan, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((list_cap + 255) / 256, c->num_cus * 4))),
                      dim3(256), 0, s, jobs, pages, list, total, sctr, T.subs, T.sub_cap, T.segpage, T.seg_cap);
-  hipLaunchKernelGGL(k_snap_seg, dim3(c->num_cus * 16), dim3(64), 0, s, jobs, pages, T.segpage, sctr + 1, T.seg_cap, T.F);
-  hipLaunchKernelGGL(k_snap_link, dim3(c->num_cus * 4), dim3(64), 0, s, jobs, pages, list, total, T.subs, T.F);
+  hipLaunchKernelGGL(k_snap_seg, dim3(c->num_cus * c->seg_waves), dim3(64), 0, s, jobs, pages, T.segpage, sctr + 1, T.seg_cap, T.F);
+  hipLaunchKernelGGL(k_snap_link, dim3(c->num_cus * c->link_waves), dim3(64), 0, s, jobs, pages, list, total, T.subs, T.F);
   hipLaunchKernelGGL(k_snap_decode, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, T.subs, sctr, T.sub_cap, q_split,
                      scratch);
   hipLaunchKernelGGL(k_snappy, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, list, total, q_serial, scratch);
@@ -628,7 +634,7 @@ static int launch_pipeline(pqg_ctx* c) {
   // stages with no possible work are not launched (the host knows each job's
   // type and levels; the kernels' own flags stay as the backstop)
   if (c->any_levels)
-    hipLaunchKernelGGL(k_level_long, dim3(qgrid(c->num_cus * 8)), dim3(64), 0, s, pages, ctr, llong, llc, lpieces, lpc,
+    hipLaunchKernelGGL(k_level_long, dim3(qgrid(c->num_cus * c->levlong_waves)), dim3(64), 0, s, pages, ctr, llong, llc, lpieces, lpc,
                        Q(kQueueLevLong));
   if (c->timed) hipEventRecord(c->ev[4], s);
   const unsigned walk_blocks = (unsigned)std::max<int64_t>(

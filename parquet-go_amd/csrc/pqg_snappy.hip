@@ -203,6 +203,24 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, int from_lane) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(from_lane << 2, (int)v);
 }
 
+// The chain step of the tag at window position rel (lo, hw: its bytes 0..7),
+// branch-free and in 32 bits: J = parse_tag_bytes' next saturated at
+// 0x7fffffff, O = its len saturated at 2^30 (the chain walks' caps).  The
+// branchy 64-bit parse costs the walk its exec-mask juggling per step.
+__device__ __forceinline__ void tag_step32(uint32_t lo, uint32_t hw, uint32_t rel, uint32_t& J, uint32_t& O) {
+  const uint32_t tag = lo & 0xff, ty = tag & 3, x = tag >> 2;
+  const uint32_t w4 = (lo >> 8) | (hw << 24);  // bytes 1..4
+  const uint32_t nb = x >= 60 ? x - 59 : 0u;    // literal: extra length bytes
+  const uint32_t mask = nb >= 4 ? 0xffffffffu : (1u << (8 * nb)) - 1u;
+  const uint32_t lm1 = x < 60 ? x : (w4 & mask);  // literal length - 1
+  const uint32_t hdr = ty == 0 ? 1 + nb : ty == 1 ? 2u : ty == 2 ? 3u : 5u;
+  const uint32_t s = rel + hdr + 1 + lm1;          // literal: the next tag (may wrap)
+  const bool sat = s < lm1 || s > 0x7fffffffu;
+  const uint32_t Jl = sat ? 0x7fffffffu : s, Ol = lm1 >= (1u << 30) - 1 ? (1u << 30) : lm1 + 1;
+  J = ty == 0 ? Jl : rel + hdr;
+  O = ty == 0 ? Ol : ty == 1 ? 4 + (x & 7) : 1 + x;
+}
+
 // ---------------------------------------------------------------------------
 // Tag-chain walk by pointer doubling (the split of big blocks, see k_snap_seg).
 // Every lane follows its own chain position x (a block offset) to the first
@@ -236,15 +254,54 @@ __device__ void chain_walk_rd(const RD& rd, int64_t slen, int64_t hi, int64_t& x
     const int64_t p = wb + lane;
     uint32_t lo, hw;
     rd(p, lo, hw);
+#ifndef PQG_SNAP_SEG_TWO
+    uint32_t J, O;  // relative to wb
+    tag_step32(lo, hw, (uint32_t)lane, J, O);
+#else
     const Tag t = parse_tag_bytes(lo, hw, p, slen, lane);
     uint32_t J = t.next < 0x7fffffff ? (uint32_t)t.next : 0x7fffffffu;  // relative to wb
     uint32_t O = t.len < (1 << 30) ? (uint32_t)t.len : (1u << 30);
+#endif
     if (p >= hi) {  // the walk ends at the first chain position >= hi: a fixed point
       J = (uint32_t)lane;
       O = 0;
     }
+#ifndef PQG_SNAP_SEG_TWO
+    // One dword per position for the doubling: a terminal position (its next
+    // tag outside the window, or itself >= hi: a fixed point) points at
+    // itself; any other at its next tag, with that tag's output bytes (< 64
+    // bytes of header and literal to stay in the window, so <= 64 output
+    // bytes) in the bits above 8.  A round is then one ds_bpermute,
+    // V = V[ptr] + (V's own sum): ptr follows, sums add (<= 63 * 64 < 2^24);
+    // the terminal's exit and output bytes are read once at the end.  Rounds
+    // stop when every pointer has reached a terminal.
+    const bool term = p >= hi || J >= 64;
+    const uint64_t tm = __ballot(term);
+    uint32_t V = term ? (uint32_t)lane : (J | (O << 8));
 #pragma unroll
     for (int r = 0; r < 6; r++) {
+      if (!__ballot(!((tm >> (V & 63)) & 1))) break;
+      const uint32_t W = bperm(V, (int)(V & 63));
+      V = W + (V & ~0xffu);
+    }
+    const int64_t rel = x - wb;
+    const bool here = act && rel < 64;
+    const uint32_t Vx = bperm(V, here ? (int)rel : lane);
+    const int T = (int)(Vx & 63);
+    const uint32_t Jx = bperm(J, T), Ox = bperm(O, T);
+    if (here) {
+      x = wb + (int64_t)Jx;
+      acc = sat_add(acc, sat_add(Vx >> 8, Ox));
+    }
+#else
+    // positions >= hi are fixed points: a lane is done once J leaves the
+    // window or reaches one (short tags need all six rounds, long ones few)
+    const uint32_t jfix = hi - wb < 64 ? (uint32_t)(hi - wb) : 64u;
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+#ifndef PQG_SNAP_ALL_ROUNDS
+      if (!__ballot(J < jfix)) break;
+#endif
       const bool in = J < 64;
       const uint32_t Jn = bperm(J, in ? (int)J : lane), On = bperm(O, in ? (int)J : lane);
       if (in) {
@@ -259,6 +316,7 @@ __device__ void chain_walk_rd(const RD& rd, int64_t slen, int64_t hi, int64_t& x
       x = wb + (int64_t)Jx;
       acc = sat_add(acc, Ox);
     }
+#endif
   }
 }
 struct GlobalRd8 {
