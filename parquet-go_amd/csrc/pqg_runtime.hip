@@ -196,7 +196,7 @@ struct pqg_ctx {
   bool dict_walk = false; // PQG_DICT_WALK=1: k_dict_walk / k_dict_walk_g walk small pages' index streams themselves
   bool fused = false;     // PQG_FUSED=1: k_page_fused, levels + small 4-byte dictionary pages in one pass
   int seg_waves = 31;     // PQG_SEG_WAVES: k_snap_seg waves per CU (its 5 KiB of LDS allow 31; 16: C4 +10 %)
-  int levlong_waves = 8;  // PQG_LEVLONG_WAVES: k_level_long waves per CU
+  int levlong_waves = 28; // PQG_LEVLONG_WAVES: k_level_long waves per CU (66 VGPRs: 7 per SIMD; 8: C5 0.61 ms, 28: 0.32)
   int link_waves = 16;    // PQG_LINK_WAVES: k_snap_link waves per CU (one wave per big page; 4: C4 +50 %)
   DevBuf lookback;       // k_page_fused: one look-back word per page
   int snappy_per_cu = 2;  // resident k_snappy waves per CU (LDS-bound: the output history ring)
