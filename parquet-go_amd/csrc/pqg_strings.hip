@@ -1262,7 +1262,13 @@ __device__ __forceinline__ void lds_copy_l(PQG_L uint8_t* dst, const PQG_L uint8
 }
 constexpr int kSrcStage = kCopyStage + 4 * 512 + 64;  // a PLAIN round's records: chars + length prefixes
 
-__global__ void __launch_bounds__(512) k_str_copy(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total,
+// k_str_copy waves per SIMD: 4 blocks of 512 per CU (its LDS allows 4; at 8
+// waves/SIMD it keeps 64 VGPRs, 8 spilled): C4 1.01 -> 0.92 ms, C5 2.57 ->
+// 2.61 ms.  (k_str_count at 4 waves/SIMD spills 36 VGPRs: C5 0.97 -> 1.15 ms.)
+#ifndef PQG_COPY_WPE
+#define PQG_COPY_WPE 8
+#endif
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(PQG_COPY_WPE))) k_str_copy(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total,
                                                   int* queue, uint8_t* value_arena, int64_t* offs_arena) {
   __shared__ int s_t;
   __shared__ int64_t s_prev;  // page-relative end of the value before the round
