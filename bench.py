@@ -129,7 +129,7 @@ def gen_workload(key, args, rank, world):
     elif key == "c5":
         R = 8 * world  # 8 row groups per GPU (64 at 8 GPUs, the C5 file)
         rgs = list(shard.row_groups_for_rank(R, rank, world))
-        data, info = W.config_c5(row_groups=rgs, rows_per_rg=args.c5_rows_per_rg)
+        data, info = W.config_c5(row_groups=rgs, rows_per_rg=args.c5_rows_per_rg, as_array=True)
         pf = pqgpu.ParquetFile(data)
         files.append((pf, [(i, c) for i in range(len(rgs)) for c in range(pf.num_columns)], ("c5", info)))
         desc = ("C5 shard: row groups %s of %d (RG i -> GPU floor(i*%d/%d)), %d rows each: LIST<double> + int32, "
@@ -303,12 +303,17 @@ def cpu_baseline(wl, seconds):
 
 
 # ---------------------------------------------------------------- PMC traffic (committed passes)
-STAGE_KERNELS = {"scan": ["k_tile_jobs", "k_page_cands", "k_cand_parse", "k_tile_scan", "k_cand_link", "k_page_chain",
-                          "k_scan_pages"], "list": ["k_page_list"], "snappy": ["k_snap_plan", "k_snap_seg", "k_snap_link", "k_snap_decode", "k_snappy",
-                                                     "k_inflate"], "levels": ["k_page_levels"],
-                 "walk": ["k_hybrid_walk"], "unused": [], "nn_scan": ["k_nn_scan"],
-                 "values": ["k_values", "k_dict_plan", "k_dict4", "k_dict_walk"], "strings": ["k_str_dict", "k_str_plain", "k_str_count", "k_char_scan",
-                                                  "k_str_copy"],
+# every kernel each stage timer brackets (pqg_runtime.hip launch_pipeline; a
+# name matches kernels it prefixes: k_page_levels covers k_page_levels_w1)
+STAGE_KERNELS = {"scan": ["k_scan_pages", "k_tile_jobs", "k_page_cands", "k_cand_parse", "k_tile_scan", "k_cand_link",
+                          "k_page_chain"],
+                 "list": ["k_page_list"],
+                 "snappy": ["k_snap_plan", "k_snap_seg", "k_snap_link", "k_snap_decode", "k_snappy", "k_inflate"],
+                 "levels": ["k_dict_resolve", "k_page_levels", "k_level_long"],
+                 "walk": ["k_hybrid_walk", "k_walk_long"], "unused": [], "nn_scan": ["k_nn_scan"],
+                 "values": ["k_values", "k_dict_plan", "k_dict4"],
+                 "strings": ["k_str_dict", "k_str_plain", "k_str_count", "k_str_delta", "k_char_scan", "k_str_copy",
+                             "k_str_dba"],
                  "finalize": ["k_finalize"]}
 
 
@@ -427,6 +432,10 @@ def run_workload(wl, decs, args, steps, warmup, barrier, dist, world, rank, cpu_
     dom = int(np.argmax(stage_ms))
     dom_name = STAGES[dom]
     achieved = alg[dom_name] / (stage_ms[dom] * 1e-3) / 1e9 if stage_ms[dom] > 0 else 0.0
+    # the decompression stage runs k_inflate for GZIP chunks, the snappy kernels otherwise
+    gz = wl.key == "c3_gzip"
+    dom_label = ("inflate" if gz else "snappy") if dom_name == "snappy" else dom_name
+    dom_kernels = [k for k in STAGE_KERNELS[dom_name] if dom_name != "snappy" or (k == "k_inflate") == gz]
     out = {
         "workload": wl.desc,
         "value": round(b_out * world / elapsed * steps / 1e9, 3),
@@ -439,12 +448,12 @@ def run_workload(wl, decs, args, steps, warmup, barrier, dist, world, rank, cpu_
         "h2d_bytes_per_rank": wl.uploaded,
         "roofline": {
             "bound": "hbm",
-            "kernel": "stage " + dom_name + " (" + "+".join(STAGE_KERNELS[dom_name]) + ")",
+            "kernel": "stage " + dom_label + " (" + "+".join(dom_kernels) + ")",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(wl.key, STAGE_KERNELS[dom_name], wl.desc),
+            "traffic": pmc_traffic(wl.key, dom_kernels, wl.desc),
             "alg_bytes_per_launch": alg[dom_name],
             "kernel_ms": round(float(stage_ms[dom]), 4),
             "measured_on": "one context (all chunks on one stream), instrumented steps after the timed ones",
@@ -540,6 +549,29 @@ def k8_list_c5(dec, wl, res, args):
     if not args.no_verify:
         out["verified"] = bool(ok)
     return out
+
+
+def compact_line(out):
+    """The bench line without its bulky fields: the headline's roofline and
+    CPU baseline, and per config value / ms per step / dominant-stage and
+    pipeline roofline fractions / bit-exactness."""
+    keep_roof = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms", "pipeline_frac")
+    c = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                             "higher_is_better", "scaling", "vs_baseline", "dtype", "data")}
+    c["config"] = {"workload": "C2: optional INT32 x 7 dictionary widths (see the full line above)",
+                   "parallelism": out["config"]["parallelism"]}
+    c["roofline"] = {k: out["roofline"][k] for k in keep_roof if k in out["roofline"]}
+    cb = out.get("cpu_baseline") or {}
+    c["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind") if k in cb} or None
+    c["verified_bit_exact"] = out.get("verified_bit_exact")
+    c["configs"] = {k: {"value": v["value"], "ms_per_step": v["ms_per_step"],
+                        "frac": v["roofline"]["frac"], "dominant": v["roofline"]["kernel"].split(" (")[0],
+                        "pipeline_frac": v["roofline"]["pipeline_frac"],
+                        "verified_bit_exact": v.get("verified_bit_exact"),
+                        "cpu_1thread": (v.get("cpu_baseline") or {}).get("value")}
+                    for k, v in out["configs"].items()}
+    c["compact"] = True
+    return c
 
 
 def launch_ranks(n):
@@ -674,6 +706,9 @@ def main():
             "configs": subs,
         }
         print(json.dumps(out), flush=True)
+        # the same line again, compact, LAST: every config's numbers survive a
+        # truncated stdout tail (the full line above carries the details)
+        print(json.dumps(compact_line(out)), flush=True)
     for d in decs:
         d.close()
     if dist is not None:

@@ -610,14 +610,44 @@ typedef struct pqw_column {
   int64_t num_slots, num_values;
 } pqw_column;
 
-// Write a whole file: `ncols` columns of `num_rows` rows split into
-// `row_groups` row groups of equal row counts.  Returns 0 and a malloc'ed
-// buffer in *out.
-int pqw_write_file(const pqw_column* cols, int ncols, int64_t num_rows, int row_groups, uint8_t** out,
-                   int64_t* out_len) {
-  Buf file;
-  file.insert(file.end(), {'P', 'A', 'R', '1'});
+}  // extern "C"
+
+namespace {
+// An open file: the bytes so far, the column specs (metadata only: their
+// array pointers are not kept past the call that wrote them) and every row
+// group's chunk records, for the footer.
+struct Writer {
+  // the bytes so far, in one malloc'ed block grown by realloc (large blocks
+  // are remapped, not copied), handed to the caller as the file at the end
+  uint8_t* mem = nullptr;
+  size_t len = 0, cap = 0;
+  std::vector<ColSpec> cs;
+  std::vector<std::vector<ChunkOut>> rgs;
+  std::vector<int64_t> rg_rows;
+  int64_t num_rows = 0;
+  Buf tail;  // footer + length + magic (build_tail)
+  ~Writer() { free(mem); }
+  bool append(const uint8_t* p, size_t n) {
+    if (len + n > cap) {
+      size_t nc = cap ? cap : 1 << 20;
+      while (nc < len + n) nc += nc / 2 + (1 << 20);
+      uint8_t* m = (uint8_t*)realloc(mem, nc);
+      if (!m) return false;
+      mem = m;
+      cap = nc;
+    }
+    memcpy(mem + len, p, n);
+    len += n;
+    return true;
+  }
+};
+
+// Append `row_groups` row groups of equal row counts holding the `ncols`
+// columns' `num_rows` rows.  A later call must pass the same columns (name,
+// type, repetition, codec).
+int add_row_groups(Writer& w, const pqw_column* cols, int ncols, int64_t num_rows, int row_groups) {
   if (row_groups < 1) row_groups = 1;
+  if (!w.cs.empty() && (int)w.cs.size() != ncols) return -3;
   std::vector<ColSpec> cs((size_t)ncols);
   std::vector<std::vector<int64_t>> row_start_slots((size_t)ncols);
   std::vector<std::vector<int64_t>> value_before_slot((size_t)ncols);
@@ -642,6 +672,10 @@ int pqw_write_file(const pqw_column* cols, int ncols, int64_t num_rows, int row_
     c.min_rle = p.min_rle > 0 ? p.min_rle : 8;
     c.v2_uncompressed_flag = p.v2_uncompressed_flag;
     c.hybrid_groups = p.hybrid_groups;
+    if (!w.cs.empty()) {
+      const ColSpec& o = w.cs[(size_t)k];
+      if (o.name != c.name || o.type != c.type || o.repetition != c.repetition || o.codec != c.codec) return -3;
+    }
     int maxd = c.repetition == 0 ? 0 : (c.repetition == 1 ? 1 : 3);
     auto& rs = row_start_slots[(size_t)k];
     for (int64_t i = 0; i < c.num_slots; i++)
@@ -657,35 +691,53 @@ int pqw_write_file(const pqw_column* cols, int ncols, int64_t num_rows, int row_
     vb[(size_t)c.num_slots] = acc;
     if (acc != c.num_values) return -2;
   }
-  std::vector<std::vector<ChunkOut>> rgs((size_t)row_groups);
-  std::vector<int64_t> rg_rows((size_t)row_groups);
   int64_t per = (num_rows + row_groups - 1) / row_groups;
+  Buf rg;  // one row group's chunks (offsets rebased onto the file below)
   for (int g = 0; g < row_groups; g++) {
     int64_t r0 = g * per, r1 = (g + 1) * per < num_rows ? (g + 1) * per : num_rows;
     if (r0 > r1) r0 = r1;
-    rg_rows[(size_t)g] = r1 - r0;
+    w.rg_rows.push_back(r1 - r0);
+    w.rgs.emplace_back();
+    rg.clear();
     for (int k = 0; k < ncols; k++) {
       auto& rs = row_start_slots[(size_t)k];
       int64_t s0 = r0 < (int64_t)rs.size() ? rs[(size_t)r0] : cs[(size_t)k].num_slots;
       int64_t s1 = r1 < (int64_t)rs.size() ? rs[(size_t)r1] : cs[(size_t)k].num_slots;
       std::vector<int64_t> starts(rs.begin() + r0, rs.begin() + r1);
       auto& vb = value_before_slot[(size_t)k];
-      rgs[(size_t)g].push_back(write_chunk(file, cs[(size_t)k], s0, s1, vb[(size_t)s0], vb[(size_t)s1], starts));
+      ChunkOut co = write_chunk(rg, cs[(size_t)k], s0, s1, vb[(size_t)s0], vb[(size_t)s1], starts);
+      co.start += (int64_t)w.len;
+      co.data_off += (int64_t)w.len;
+      if (co.dict_off >= 0) co.dict_off += (int64_t)w.len;
+      w.rgs.back().push_back(co);
     }
+    if (!w.append(rg.data(), rg.size())) return -4;
   }
-  // footer: FileMetaData
+  w.num_rows += num_rows;
+  if (w.cs.empty()) {
+    for (ColSpec& c : cs) c.values = nullptr, c.offsets = nullptr, c.def_levels = c.rep_levels = nullptr;
+    w.cs = cs;
+  }
+  return 0;
+}
+
+// The footer (FileMetaData), its length and the closing magic into w.tail.
+void build_tail(Writer& w) {
+  const std::vector<ColSpec>& cs = w.cs;
+  const int ncols = (int)cs.size();
+  const int row_groups = (int)w.rgs.size();
   Buf meta;
   TW t(meta);
   t.i32(1, 1);
   // schema: root + leaves (LIST columns expand to 3 elements + the leaf)
   int64_t n_elems = 1;
-  for (auto& c : cs) n_elems += c.repetition == 2 ? 3 : 1;
+  for (const auto& c : cs) n_elems += c.repetition == 2 ? 3 : 1;
   t.list(2, 12, n_elems);
   t.begin_struct_elem();
   t.str(4, "schema");
   t.i32(5, ncols);
   t.end_struct();
-  for (auto& c : cs) {
+  for (const auto& c : cs) {
     if (c.repetition == 2) {
       t.begin_struct_elem();
       t.i32(3, 1);  // OPTIONAL
@@ -714,14 +766,14 @@ int pqw_write_file(const pqw_column* cols, int ncols, int64_t num_rows, int row_
       t.end_struct();
     }
   }
-  t.i64(3, num_rows);
+  t.i64(3, w.num_rows);
   t.list(4, 12, row_groups);
   for (int g = 0; g < row_groups; g++) {
     t.begin_struct_elem();
     t.list(1, 12, ncols);
     int64_t total = 0;
     for (int k = 0; k < ncols; k++) {
-      ChunkOut& co = rgs[(size_t)g][(size_t)k];
+      const ChunkOut& co = w.rgs[(size_t)g][(size_t)k];
       const ColSpec& c = cs[(size_t)k];
       total += co.tus;
       t.begin_struct_elem();
@@ -751,19 +803,69 @@ int pqw_write_file(const pqw_column* cols, int ncols, int64_t num_rows, int row_
       t.end_struct();
     }
     t.i64(2, total);
-    t.i64(3, rg_rows[(size_t)g]);
+    t.i64(3, w.rg_rows[(size_t)g]);
     t.end_struct();
   }
   t.str(6, "pqgpu-gen");
   t.stop();
-  file.insert(file.end(), meta.begin(), meta.end());
-  put_u32(file, (uint32_t)meta.size());
-  file.insert(file.end(), {'P', 'A', 'R', '1'});
-  *out = (uint8_t*)malloc(file.size());
-  memcpy(*out, file.data(), file.size());
-  *out_len = (int64_t)file.size();
+  w.tail = meta;
+  put_u32(w.tail, (uint32_t)meta.size());
+  w.tail.insert(w.tail.end(), {'P', 'A', 'R', '1'});
+}
+}  // namespace
+
+extern "C" {
+
+// Write a whole file: `ncols` columns of `num_rows` rows split into
+// `row_groups` row groups of equal row counts.  Returns 0 and a malloc'ed
+// buffer in *out.
+int pqw_write_file(const pqw_column* cols, int ncols, int64_t num_rows, int row_groups, uint8_t** out,
+                   int64_t* out_len) {
+  Writer w;
+  const uint8_t magic[4] = {'P', 'A', 'R', '1'};
+  if (!w.append(magic, 4)) return -4;
+  const int rc = add_row_groups(w, cols, ncols, num_rows, row_groups);
+  if (rc) return rc;
+  build_tail(w);
+  if (!w.append(w.tail.data(), w.tail.size())) return -4;
+  *out = w.mem;
+  *out_len = (int64_t)w.len;
+  w.mem = nullptr;
   return 0;
 }
+
+// A file written one row group at a time, so a caller never holds more than
+// one row group's column arrays (the C5 shard: 8 row groups per rank):
+// pqw_writer_new, pqw_writer_add (one call per row group, the same columns
+// each time), pqw_writer_finish (the footer; the file's malloc'ed bytes are
+// handed over, free them with pqw_free; the writer is freed).
+void* pqw_writer_new() {
+  Writer* w = new Writer();
+  const uint8_t magic[4] = {'P', 'A', 'R', '1'};
+  if (!w->append(magic, 4)) {
+    delete w;
+    return nullptr;
+  }
+  return w;
+}
+int pqw_writer_add(void* h, const pqw_column* cols, int ncols, int64_t num_rows) {
+  return add_row_groups(*(Writer*)h, cols, ncols, num_rows, 1);
+}
+int pqw_writer_finish(void* h, uint8_t** out, int64_t* out_len) {
+  Writer* w = (Writer*)h;
+  build_tail(*w);
+  if (!w->append(w->tail.data(), w->tail.size())) {
+    delete w;
+    return -4;
+  }
+  *out = (uint8_t*)realloc(w->mem, w->len);  // shrink to the file
+  if (!*out) *out = w->mem;
+  *out_len = (int64_t)w->len;
+  w->mem = nullptr;
+  delete w;
+  return 0;
+}
+void pqw_writer_free(void* h) { delete (Writer*)h; }
 
 void pqw_free(uint8_t* p) { free(p); }
 

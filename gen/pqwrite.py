@@ -55,6 +55,12 @@ def lib():
         L.pqw_snappy_compress.restype = C.c_int64
         L.pqw_set_snappy_block.argtypes = [C.c_int64]
         L.pqw_set_snappy_block.restype = None
+        L.pqw_writer_new.argtypes = []
+        L.pqw_writer_new.restype = C.c_void_p
+        L.pqw_writer_add.argtypes = [C.c_void_p, C.POINTER(_PqwColumn), C.c_int, C.c_int64]
+        L.pqw_writer_finish.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+        L.pqw_writer_free.argtypes = [C.c_void_p]
+        L.pqw_writer_free.restype = None
         _lib = L
     return _lib
 
@@ -102,8 +108,7 @@ class Column:
         return 1 if self.repetition == LIST else 0
 
 
-def write_file(columns, num_rows, row_groups=1):
-    L = lib()
+def _pqw_columns(columns):
     arr = (_PqwColumn * len(columns))()
     names = []
     for i, c in enumerate(columns):
@@ -121,6 +126,12 @@ def write_file(columns, num_rows, row_groups=1):
         a.def_levels = c.def_levels.ctypes.data if c.def_levels is not None else None
         a.rep_levels = c.rep_levels.ctypes.data if c.rep_levels is not None else None
         a.num_slots, a.num_values = c.num_slots, c.num_values
+    return arr, names
+
+
+def write_file(columns, num_rows, row_groups=1):
+    L = lib()
+    arr, names = _pqw_columns(columns)
     out = C.c_void_p()
     n = C.c_int64()
     rc = L.pqw_write_file(arr, len(columns), num_rows, row_groups, C.byref(out), C.byref(n))
@@ -130,6 +141,41 @@ def write_file(columns, num_rows, row_groups=1):
     data = np.ctypeslib.as_array(C.cast(out, C.POINTER(C.c_uint8)), shape=(n.value,)).tobytes()
     L.pqw_free(out)
     return data
+
+
+class RowGroupWriter:
+    """A file written one row group at a time (pqw_writer_*): the caller builds
+    one row group's columns, add()s them and drops them, so it never holds
+    more than one row group's arrays.  finish() returns the file as a numpy
+    uint8 array (one copy of the bytes; ParquetFile takes it without copying)."""
+
+    def __init__(self):
+        self._h = lib().pqw_writer_new()
+
+    def add(self, columns, num_rows):
+        arr, names = _pqw_columns(columns)
+        rc = lib().pqw_writer_add(self._h, arr, len(columns), num_rows)
+        if rc != 0:
+            raise ValueError("pqw_writer_add failed: %d" % rc)
+
+    def finish(self):
+        import weakref
+        L = lib()
+        out = C.c_void_p()
+        n = C.c_int64()
+        rc = L.pqw_writer_finish(self._h, C.byref(out), C.byref(n))
+        self._h = None
+        if rc != 0:
+            raise ValueError("pqw_writer_finish failed: %d" % rc)
+        # the writer's own buffer, freed when the array (and every view of it) is gone
+        arr = np.ctypeslib.as_array(C.cast(out, C.POINTER(C.c_uint8)), shape=(n.value,))
+        weakref.finalize(arr, L.pqw_free, out.value)
+        return arr
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().pqw_writer_free(self._h)
+            self._h = None
 
 
 def hybrid_encode(values, width, min_rle=8):
@@ -388,25 +434,8 @@ def c5_row_group_columns(rg, rows, seed=5, rows_per_page=20000):
     return out
 
 
-def config_c5(row_groups=(0,), rows_per_rg=C5_ROWS_PER_RG, seed=5, rows_per_page=20000):
-    """C5 row groups `row_groups` (global indices of the 64-row-group file; one
-    rank's shard under RG i -> GPU floor(i * G / 64)) written as one file, in
-    order.  Returns (file bytes, info)."""
-    parts = [c5_row_group_columns(rg, rows_per_rg, seed, rows_per_page) for rg in row_groups]
-
-    def cat(name, key):
-        arrs = [p[name].get(key) for p in parts]
-        if arrs[0] is None:
-            return None
-        if key == "offsets":
-            res, base = [np.zeros(1, np.int64)], 0
-            for a in arrs:
-                res.append(a[1:] + base)
-                base += int(a[-1])
-            return np.concatenate(res)
-        return np.concatenate(arrs)
-
-    rows = rows_per_rg * len(parts)
+def c5_columns(p, rows_per_rg, rows_per_page=20000):
+    """The nine C5 Column objects of one row group's arrays `p`."""
     rpp_d = _dbp_safe_rows_per_page(rows_per_rg, rows_per_page)
     # Quirk-free by construction (SURVEY §8a): the reference appends each page's
     # whole numValues-long slice to the column store, trailing nils included
@@ -420,23 +449,41 @@ def config_c5(row_groups=(0,), rows_per_rg=C5_ROWS_PER_RG, seed=5, rows_per_page
     # each (hybridEncoder.bpEncode, hybrid_encoder.go:59-73).  The columns
     # without nulls keep pyarrow's 20 000 rows per page.
     one = dict(rows_per_page=rows_per_rg, hybrid_groups=REF_HYBRID)
-    cols = [
-        Column("lst", DOUBLE, cat("lst", "values"), repetition=LIST, def_levels=cat("lst", "def_levels"),
-               rep_levels=cat("lst", "rep_levels"), **one),
-        Column("i32", INT32, cat("i32", "values"), rows_per_page=rows_per_page),
-        Column("i64d", INT64, cat("i64d", "values"), encoding=DELTA_BINARY_PACKED, rows_per_page=rpp_d),
-        Column("f64", DOUBLE, cat("f64", "values"), rows_per_page=rows_per_page),
-        Column("f32", FLOAT, cat("f32", "values"), rows_per_page=rows_per_page),
-        Column("i96", INT96, cat("i96", "values"), rows_per_page=rows_per_page),
+    return [
+        Column("lst", DOUBLE, p["lst"]["values"], repetition=LIST, def_levels=p["lst"]["def_levels"],
+               rep_levels=p["lst"]["rep_levels"], **one),
+        Column("i32", INT32, p["i32"]["values"], rows_per_page=rows_per_page),
+        Column("i64d", INT64, p["i64d"]["values"], encoding=DELTA_BINARY_PACKED, rows_per_page=rpp_d),
+        Column("f64", DOUBLE, p["f64"]["values"], rows_per_page=rows_per_page),
+        Column("f32", FLOAT, p["f32"]["values"], rows_per_page=rows_per_page),
+        Column("i96", INT96, p["i96"]["values"], rows_per_page=rows_per_page),
         # the optional int32 column is written with dictionary off (PLAIN)
-        Column("oi32", INT32, cat("oi32", "values"), repetition=OPTIONAL, encoding=PLAIN,
-               def_levels=cat("oi32", "def_levels"), **one),
-        Column("s", BYTE_ARRAY, cat("s", "values"), offsets=cat("s", "offsets"), encoding=RLE_DICTIONARY, **one),
-        Column("i64s", INT64, cat("i64s", "values"), codec=SNAPPY, rows_per_page=rows_per_page),
+        Column("oi32", INT32, p["oi32"]["values"], repetition=OPTIONAL, encoding=PLAIN,
+               def_levels=p["oi32"]["def_levels"], **one),
+        Column("s", BYTE_ARRAY, p["s"]["values"], offsets=p["s"]["offsets"], encoding=RLE_DICTIONARY, **one),
+        Column("i64s", INT64, p["i64s"]["values"], codec=SNAPPY, rows_per_page=rows_per_page),
     ]
-    data = write_file(cols, rows, row_groups=len(parts))
-    del cols, parts
+
+
+def config_c5(row_groups=(0,), rows_per_rg=C5_ROWS_PER_RG, seed=5, rows_per_page=20000, as_array=False):
+    """C5 row groups `row_groups` (global indices of the 64-row-group file; one
+    rank's shard under RG i -> GPU floor(i * G / 64)) written as one file, in
+    order, ONE ROW GROUP AT A TIME: a row group's arrays are generated, written
+    and dropped before the next (row groups are independent,
+    chunk_reader.go:404-431), so a rank holds its file plus one row group's
+    arrays, not its whole shard's.  Returns (file bytes, info); as_array: the
+    file as a numpy uint8 array (no bytes copy: the bench's multi-GB shard)."""
     rgs = list(row_groups)
+    wr = RowGroupWriter()
+    for rg in rgs:
+        p = c5_row_group_columns(rg, rows_per_rg, seed, rows_per_page)
+        cols = c5_columns(p, rows_per_rg, rows_per_page)
+        wr.add(cols, rows_per_rg)
+        del cols, p
+    data = wr.finish()
+    if not as_array:
+        data = data.tobytes()
+    rows = rows_per_rg * len(rgs)
 
     def part(i):
         """Expected arrays of the file's row group i, regenerated (the same seeds):

@@ -436,8 +436,11 @@ __device__ __forceinline__ void dict_items(PageDev* pages, const int* total, int
     VRec r;
     r.job = -1;
     if (t < nt) r = recs[t];
-    const int own = kMode == 0   ? (r.n_blocks >= 0 && !(big && big_dict(r)))
-                    : kMode == 3 ? (r.n_blocks >= 0 && big_dict(r))
+    // a zero-width page (key 0 for every value, no run table) stays with
+    // k_dict4 whatever its dictionary's size: k_dict_plan raises the big-dict
+    // stage flag only for pages with index streams
+    const int own = kMode == 0   ? (r.n_blocks >= 0 && !(big && r.w > 0 && big_dict(r)))
+                    : kMode == 3 ? (r.n_blocks >= 0 && r.w > 0 && big_dict(r))
                     : kMode == 1 ? (r.n_blocks == -1)
                                  : (r.n_blocks == -2);
     if (!own) r.job = -1;  // another kernel's page

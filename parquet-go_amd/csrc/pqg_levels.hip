@@ -21,6 +21,8 @@
 #include "pqg_device.h"
 #include "pqg_hybrid.h"
 #include "pqg_levdec.h"
+#include "pqg_lev1.h"
+#include <type_traits>
 
 namespace pqg {
 
@@ -402,11 +404,27 @@ __global__ void __launch_bounds__(64) k_level_long(PageDev* pages, const int* ct
 // on one list, each taking its own jobs' pages (0: this kernel takes all).
 __device__ __forceinline__ bool w1_job(const JobDev& job) { return job.max_rep == 0 && job.max_def <= 1; }
 
+// k_page_levels_w1's LDS: the whole-page decoder's window and table, or the
+// batch decoder's (pages the whole-page decoder does not take)
+union LevW1Shared {
+  LevShared lev;
+  Lev1Shared l1;
+};
+template <bool kW1>
+using LevelsShared = typename std::conditional<kW1, LevW1Shared, LevShared>::type;
+__device__ __forceinline__ LevShared& lev_sh(LevShared& s) { return s; }
+__device__ __forceinline__ LevShared& lev_sh(LevW1Shared& s) { return s.lev; }
+
+// split: bit 0 = both kernels run on one list, each taking its own jobs'
+// pages; bit 1 (w = 1 kernel) = the whole-page decoder first (pqg_lev1.h)
 template <bool kW1>
 __device__ __forceinline__ void page_levels(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                                             uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena,
-                                            LongLev* longs, int long_cap, LevPiece* pieces, int piece_cap, int split) {
-  __shared__ __attribute__((aligned(16))) LevShared sh;
+                                            LongLev* longs, int long_cap, LevPiece* pieces, int piece_cap, int split_flags) {
+  __shared__ __attribute__((aligned(16))) LevelsShared<kW1> shu;
+  LevShared& sh = lev_sh(shu);
+  const int split = split_flags & 1;
+  const bool whole = kW1 && (split_flags & 2);
   const int lane = lane_id();
   const LongTables lt{longs, pieces, const_cast<int*>(total), long_cap, piece_cap};
   for (;;) {
@@ -441,10 +459,18 @@ __device__ __forceinline__ void page_levels(JobDev* jobs, PageDev* pages, const 
         if (job.max_def > 0) {
           if (ps.def_n < 0) de = kLEVELS;
           else {
-            uint32_t c;
-            de = level_stream<kW1>(ps.def, ps.def_n, bits_len((uint32_t)job.max_def), (uint32_t)n,
-                                   gmut(def_arena) + job.slot_base + pg.slot_offset, (uint32_t)job.max_def, sh, &c, lt,
-                                   pidx);
+            uint32_t c = 0;
+            bool done = false;
+            if constexpr (kW1) {
+              if (whole && job.max_def == 1 && ps.def_n <= kL1MaxN)
+                done = lev1_page(ps.def, (uint32_t)ps.def_n, (uint32_t)n,
+                                 gmut(def_arena) + job.slot_base + pg.slot_offset, shu.l1, &c);
+            }
+            if (done) de = kOK;
+            else
+              de = level_stream<kW1>(ps.def, ps.def_n, bits_len((uint32_t)job.max_def), (uint32_t)n,
+                                     gmut(def_arena) + job.slot_base + pg.slot_offset, (uint32_t)job.max_def, sh, &c,
+                                     lt, pidx);
             nn = c;
           }
         } else {
@@ -468,7 +494,7 @@ __global__ void __launch_bounds__(64, PQG_LEVELS_WPE) k_page_levels(JobDev* jobs
 }
 
 #ifndef PQG_LEVELS_W1_WPE
-#define PQG_LEVELS_W1_WPE 8
+#define PQG_LEVELS_W1_WPE 4
 #endif
 __global__ void __launch_bounds__(64, PQG_LEVELS_W1_WPE) k_page_levels_w1(JobDev* jobs, PageDev* pages, const int* list,
                                                        const int* total, int* queue, uint8_t* scratch,

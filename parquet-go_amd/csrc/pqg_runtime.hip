@@ -194,6 +194,7 @@ struct pqg_ctx {
   bool stride = true;     // the K1 stride walk of equal-page chunks (PQG_STRIDE=0: the candidate scan takes them)
   bool dict_big = true;   // k_dict4_big for dictionaries past 4096 entries (PQG_DICT_BIG=0: k_dict4 gathers them)
   bool dict_walk = false; // PQG_DICT_WALK=1: k_dict_walk / k_dict_walk_g walk small pages' index streams themselves
+  bool lev1 = true;       // the whole-page 1-bit level decoder in k_page_levels_w1 (PQG_LEV1=0: the batch decoder alone)
   bool fused = false;     // PQG_FUSED=1: k_page_fused, levels + small 4-byte dictionary pages in one pass
   int seg_waves = 31;     // PQG_SEG_WAVES: k_snap_seg waves per CU (its 5 KiB of LDS allow 31; 16: C4 +10 %)
   int levlong_waves = 28; // PQG_LEVLONG_WAVES: k_level_long waves per CU (66 VGPRs: 7 per SIMD; 8: C5 0.61 ms, 28: 0.32)
@@ -290,6 +291,7 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
   if (const char* e = getenv("PQG_STRIDE")) c->stride = atoi(e) != 0;
   if (const char* e = getenv("PQG_WALK_WAVE")) c->walk_wave = atoi(e) != 0;
   if (const char* e = getenv("PQG_FUSED")) c->fused = atoi(e) != 0;
+  if (const char* e = getenv("PQG_LEV1")) c->lev1 = atoi(e) != 0;
   if (const char* e = getenv("PQG_SEG_WAVES")) c->seg_waves = atoi(e) > 0 ? atoi(e) : c->seg_waves;
   if (const char* e = getenv("PQG_LEVLONG_WAVES")) c->levlong_waves = atoi(e) > 0 ? atoi(e) : c->levlong_waves;
   if (const char* e = getenv("PQG_LINK_WAVES")) c->link_waves = atoi(e) > 0 ? atoi(e) : c->link_waves;
@@ -625,7 +627,7 @@ static int launch_pipeline(pqg_ctx* c) {
     if (any_w1)
       hipLaunchKernelGGL(k_page_levels_w1, dim3(qgrid(c->num_cus * 32)), dim3(64), 0, s, jobs, pages, list, ctr, Q(1),
                          scratch, streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p, llong, llc, lpieces, lpc,
-                         split);
+                         split | (c->lev1 ? 2 : 0));
     if (any_gen)
       hipLaunchKernelGGL(k_page_levels, dim3(qgrid(c->num_cus * 24)), dim3(64), 0, s, jobs, pages, list, ctr,
                          Q(split ? kQueueLevGen : 1), scratch, streams, (uint8_t*)c->def_arena.p,

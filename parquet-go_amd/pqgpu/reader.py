@@ -42,10 +42,15 @@ class ParquetFile:
         h = C.c_void_p()
         self.path = _path
         if _path is None:
-            self.data = bytes(data)
-            self._buf = np.frombuffer(self.data, dtype=np.uint8)
+            if isinstance(data, np.ndarray) and data.dtype == np.uint8 and data.ndim == 1 and data.flags.c_contiguous:
+                self.data = data  # a large file (the bench's C5 shard): no second copy
+                self._buf = data
+            else:
+                self.data = bytes(data)
+                self._buf = np.frombuffer(self.data, dtype=np.uint8)
             self.size = len(self.data)
-            _check(L.pqg_file_open(self.data, len(self.data), C.byref(h)), "pqg_file_open")
+            ptr = self._buf.ctypes.data if self.size else None
+            _check(L.pqg_file_open(C.cast(ptr, C.c_char_p) if ptr else b"", self.size, C.byref(h)), "pqg_file_open")
         else:
             self.data = None
             self._buf = None
@@ -183,6 +188,22 @@ class GpuDecoder:
         if arr.nbytes:
             _check(self.L.pqg_memcpy_h2d(self.ctx, p, arr.ctypes.data, arr.nbytes), "pqg_memcpy_h2d")
         self._bufs.append(p)
+        return p.value
+
+    def upload_ranges(self, buf, ranges):
+        """One device buffer holding buf[lo:hi] for each (lo, hi) of `ranges`,
+        packed in order, copied range by range (no packed host copy)."""
+        total = sum(hi - lo for lo, hi in ranges)
+        p = C.c_void_p()
+        _check(self.L.pqg_device_alloc(self.ctx, max(total, 1), C.byref(p)), "pqg_device_alloc")
+        self._bufs.append(p)
+        at = 0
+        for lo, hi in ranges:
+            if hi > lo:
+                src = buf[lo:hi]
+                _check(self.L.pqg_memcpy_h2d(self.ctx, C.c_void_p(p.value + at), src.ctypes.data, hi - lo),
+                       "pqg_memcpy_h2d")
+            at += hi - lo
         return p.value
 
     def free(self, ptr):
@@ -329,14 +350,19 @@ def span_jobs(pf: ParquetFile, specs, dec, to_eof=()):
     Returns (jobs, device pointer, bytes uploaded)."""
     ranges, metas = chunk_ranges(pf, specs, to_eof)
     total = sum(hi - lo for lo, hi in ranges)
-    host = np.empty(max(total, 1), dtype=np.uint8)
     base = []  # packed offset of each range
     at = 0
     for lo, hi in ranges:
-        host[at:at + hi - lo] = pf.read_range(lo, hi)
         base.append(at)
         at += hi - lo
-    dev = dec.upload(host)
+    if pf._buf is not None:  # the file in host memory: each range straight from it
+        dev = dec.upload_ranges(pf._buf, ranges)
+    else:
+        host = np.empty(max(total, 1), dtype=np.uint8)
+        for (lo, hi), b in zip(ranges, base):
+            host[b:b + hi - lo] = pf.read_range(lo, hi)
+        dev = dec.upload(host)
+        del host
     jobs = []
     for (rg, c), m in zip(specs, metas):
         job = abi.ChunkJob()

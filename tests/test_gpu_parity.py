@@ -564,6 +564,17 @@ def _str_cases():
     # fixed-width short dictionary (advisor case): count > payload / width, index past the payload
     sd = U.page_header_dict(8, 8, 1000) + i32([1, 2])
     cases.append(("dict_short_fixed", sd + U.v1_page(bytes([10]) + H([999, 0], 10), 2, 8), dict(ptype=abi.INT32)))
+    # zero bit width over a dictionary of 4097..79 872 entries (advisor case): the
+    # page yields dict[0] for every value (hybrid_decoder.go:84-86), alone and
+    # next to a page that does send its keys to the big-dictionary kernel
+    bigd = np.arange(7, 7 + 5000, dtype=np.int32).tobytes()
+    bdp = U.page_header_dict(len(bigd), len(bigd), 5000) + bigd
+    cases.append(("dict_big_zero_width", bdp + U.v1_page(bytes([0]), 9, 8), dict(ptype=abi.INT32)))
+    cases.append(("dict_big_zero_width_mixed", bdp + U.v1_page(bytes([0]), 9, 8)
+                  + U.v1_page(bytes([13]) + H([4999, 0, 17, 4096], 13), 4, 8) + U.v1_page(bytes([0]), 3, 8),
+                  dict(ptype=abi.INT32)))
+    cases.append(("dict_big_zero_width_nulls", bdp + U.v1_page(bytes([0]), 6, 8, defs=H([1, 0, 1, 1, 0, 1], 1)),
+                  dict(ptype=abi.INT32, max_def=1)))
     return cases
 
 
