@@ -276,7 +276,8 @@ int pqg_get_pages(pqg_ctx* ctx, int job, pqg_page_info* out, int cap);
 int pqg_last_timings(pqg_ctx* ctx, float* out, int cap);
 
 /* Per-stage HIP events on the ctx stream (on by default): `on` = 0 records
- * none (pqg_last_timings then reports nothing new), 1 records them.  The
+ * none (pqg_last_timings then returns 0 entries until a timed decode), 1
+ * records them.  The
  * events are instrumentation: each costs a few microseconds of stream time,
  * which matters for small batches. */
 int pqg_set_timing(pqg_ctx* ctx, int on);

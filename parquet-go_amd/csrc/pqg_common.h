@@ -298,13 +298,11 @@ constexpr int kQueueStrDelta = 11;
 constexpr int kQueueStrDba = 12;
 constexpr int kQueueLevLong = 13;  // pieces of the long level runs (k_level_long)
 constexpr int kQueueInflate = 14;  // GZIP pages (k_inflate)
-constexpr int kQueueDictWalk = 15;   // small 4-byte dictionary pages walked in-kernel, LDS dictionary (k_dict_walk)
-constexpr int kQueueDictWalkG = 16;  // the same, dictionary gathered from global memory (k_dict_walk_g)
-constexpr int kQueueLevGen = 17;  // k_page_levels when k_page_levels_w1 takes the w = 1 jobs' pages
-constexpr int kQueueDictBig = 18; // k_dict4_big: run-table pages of dictionaries past 4096 entries
-constexpr int kQueueWalkWave = 19;  // k_walk_wave: one wave per value stream
-constexpr int kQueueSlots = 20;
-constexpr int kPresentBigDict = 8;  // stage flag (kModePresentOff + 8): a page for k_dict4_big  // queue regions zeroed per launch: 0-8, the stage flags (9), 10-16
+constexpr int kQueueLevGen = 15;  // k_page_levels when k_page_levels_w1 takes the w = 1 jobs' pages
+constexpr int kQueueDictBig = 16; // k_dict4_big: run-table pages of dictionaries past 4096 entries
+// queue regions zeroed per launch: 0-8, the stage flags (9), 10-16
+constexpr int kQueueSlots = 17;
+constexpr int kPresentBigDict = 8;  // stage flag (kModePresentOff + 8): a page for k_dict4_big
 
 // Scan tiles of the speculative page-header search.
 constexpr int kScanTile = 16384;

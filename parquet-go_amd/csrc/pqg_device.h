@@ -90,13 +90,6 @@ __device__ __forceinline__ int values_supported(int type, int type_length, int e
   return 0;
 }
 
-// 4-byte dictionary data pages small enough to be one values part (pqg_common.h
-// "Big pages"): k_dict4 walks their index streams itself (IdxWalk), and
-// k_hybrid_walk skips them when the launch says so.
-__device__ __forceinline__ bool dict_walk_page(const PageDev& pg) {
-  return pg.vmode == 1 && pg.num_values >= 0 && pg.num_values <= kSplitMin;
-}
-
 template <class P>
 __device__ __forceinline__ uint32_t rd_u32(P p) {
   return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;

@@ -30,9 +30,66 @@
 #include "pqg_common.h"
 #include "pqg_device.h"
 #include "pqg_hybrid.h"
-#include "pqg_idxwalk.h"
 
 namespace pqg {
+
+// inclusive prefix max over the wave (DPP row_shr 1/2/4/8, row_bcast 15/31)
+__device__ __forceinline__ uint32_t ldpp_incl_max_u32(uint32_t x) {
+  uint32_t t;
+#define PQG_MAX_STEP(ctrl, rm, bc)                                         \
+  t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, rm, 0xf, bc); \
+  x = t > x ? t : x;
+  PQG_MAX_STEP(0x111, 0xf, true) PQG_MAX_STEP(0x112, 0xf, true) PQG_MAX_STEP(0x114, 0xf, true)
+  PQG_MAX_STEP(0x118, 0xf, true) PQG_MAX_STEP(0x142, 0xa, false) PQG_MAX_STEP(0x143, 0xc, false)
+#undef PQG_MAX_STEP
+  return x;
+}
+
+// Output stores: non-temporal (streaming), so that the output stream does not
+// evict the dictionary's L2 lines (b = 20: 4 MiB, the size of one XCD's L2).
+#ifndef PQG_DICT_NT
+#define PQG_DICT_NT PQG_NT_OUT
+#endif
+#ifndef PQG_DICT_NT_IN
+#define PQG_DICT_NT_IN 1  // the index-stream stage loads non-temporal too (r04: C2 3.22 -> 3.14-3.18 ms; 0: temporal)
+#endif
+__device__ __forceinline__ void dict_store(PQG_G uint32_t* p, uint32_t v) {
+#if PQG_DICT_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
+// Dictionary entries in LDS or in global memory.  Keys >= count read entry 0;
+// the caller records the first such index (the page then fails with "dict:
+// invalid index", and its values are never used).
+struct LdsDict {
+  static constexpr bool kGlobal = false;
+  const PQG_L uint32_t* d;
+  __device__ __forceinline__ uint32_t operator()(uint32_t k) const { return d[k]; }
+};
+struct GlobalDict {
+  static constexpr bool kGlobal = true;
+  const PQG_G uint32_t* d;
+  __device__ __forceinline__ uint32_t operator()(uint32_t k) const { return d[k]; }
+};
+// A dictionary whose first n entries are in LDS and the rest in global memory
+// (k_dict4_big).  Both loads are issued for every lane (a load under a branch
+// is waited for inside it); lanes served by LDS all read global entry 0, one
+// request per wave, so only the keys past the prefix cost L2 requests.
+struct PrefixDict {
+  static constexpr bool kGlobal = true;
+  const PQG_L uint32_t* l;
+  const PQG_G uint32_t* g;
+  uint32_t n;
+  __device__ __forceinline__ uint32_t operator()(uint32_t k) const {
+    const bool in = k < n;
+    const uint32_t gv = g[in ? 0u : k];
+    const uint32_t lv = l[in ? k : 0u];
+    return in ? lv : gv;
+  }
+};
 
 #ifndef PQG_DICT_PPAY
 #define PQG_DICT_PPAY 4096
@@ -63,17 +120,15 @@ struct PieceShared {
 // LDS of a dictionary workgroup.  kMode 0: run-table pages with a dictionary
 // of <= kDictLdsEntries entries, or none (k_dict4); 3: run-table pages with a
 // larger dictionary, its first kBigLdsEntries entries in LDS (k_dict4_big, one
-// 8-wave workgroup per CU); 1: walked pages with a dictionary of <=
-// kDictLdsEntries entries (k_dict_walk); 2: walked pages gathering from global
-// memory (k_dict_walk_g: no LDS dictionary, so more workgroups fit a CU).
+// 8-wave workgroup per CU).
 constexpr int kBigWaves = 8;
 constexpr int kBigLdsEntries = 26624;  // 104 KiB: with 8 waves' page stages, one workgroup per CU
 template <int kMode>
 constexpr int dict_waves() { return kMode == 3 ? kBigWaves : kDWaves; }
 template <int kMode>
 struct DictShared {
-  uint32_t dict[kMode == 2 ? 1 : kMode == 3 ? kBigLdsEntries : kDictLdsEntries];
-  typename std::conditional<kMode == 0 || kMode == 3, PieceShared, WalkShared>::type w[dict_waves<kMode>()];
+  uint32_t dict[kMode == 3 ? kBigLdsEntries : kDictLdsEntries];
+  PieceShared w[dict_waves<kMode>()];
   const uint8_t* dict_ptr;          // the dictionary being staged (set by a wave that holds its VRec)
   int dict_cnt;
   int item;
@@ -321,11 +376,9 @@ __device__ __forceinline__ bool big_dict(const VRec& r) {
 // byte, > 32 is an error).
 // One VRec per work item (a page's part, k_part_plan): a part of a big page is
 // its blocks [b0, next part's b0) and values [v0, next part's v0).
-// walk_small: pages of <= kSplitMin values were not walked by k_hybrid_walk
-// (dict_walk_page): k_dict_walk / k_dict_walk_g walk their streams (VRec.n_blocks < 0).
 __global__ void __launch_bounds__(256) k_dict_plan(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total,
                                                    uint8_t* value_arena, const HStream* streams, const RunEnt* runs,
-                                                   const BlockDesc* blks, VRec* recs, int walk_small) {
+                                                   const BlockDesc* blks, VRec* recs) {
   if (total[kModePresentOff + 1] == 0) return;
   const int nt = min(total[kCtrItems], total[kCtrPartsCap]);
   for (int t = blockIdx.x * 256 + threadIdx.x; t < nt; t += gridDim.x * 256) {
@@ -336,8 +389,7 @@ __global__ void __launch_bounds__(256) k_dict_plan(JobDev* jobs, PageDev* pages,
     const int pidx = pr.pidx;
     r.pidx = pidx;
     PageDev& P = pages[pidx];
-    if (pr.vmode == 1 && P.read_status == kOK && (P.page_type == 0 || P.page_type == 3) && P.vmode == 1 &&
-        !(P.flags & kPageFused)) {
+    if (pr.vmode == 1 && P.read_status == kOK && (P.page_type == 0 || P.page_type == 3) && P.vmode == 1) {
       const JobDev& J = jobs[P.job];
       if (J.status != kCAPACITY) {
         int re = kOK, dw = 0;
@@ -354,18 +406,7 @@ __global__ void __launch_bounds__(256) k_dict_plan(JobDev* jobs, PageDev* pages,
           r.dcount = J.dict_data ? (int32_t)J.dict_count : 0;
           r.nn = P.not_null;
           r.w = dw;
-          if (dw > 0 && walk_small && dict_walk_page(P)) {
-            const HStream& S = streams[P.hs_val];
-            r.p = S.p;
-            r.n = (int32_t)S.n;
-            r.runs = nullptr;  // walked in k_dict_walk
-            r.blks = nullptr;
-            // k_dict_walk: a dictionary that fits LDS; k_dict_walk_g: any other
-            r.n_blocks = (r.dict && r.dcount >= 1 && r.dcount <= kDictLdsEntries) ? -1 : -2;
-            r.count = r.nn;
-            r.produced = r.nn;
-            r.serr = kOK;
-          } else if (dw > 0) {
+          if (dw > 0) {
             const HStream& S = streams[P.hs_val];
             const bool last = pr.p + 1 >= pr.np;
             const int b1 = last ? S.n_blocks : parts[t + 1].b0;
@@ -390,10 +431,8 @@ __global__ void __launch_bounds__(256) k_dict_plan(JobDev* jobs, PageDev* pages,
 
 // Mode 1 pages (4-byte dictionary columns): the C2 path, kDWaves * 64 threads
 // per workgroup taking kDWaves consecutive work items.  kMode (DictShared):
-// 0 = pages with run tables (k_dict4), 1 / 2 = small pages whose index
-// streams are walked here (k_dict_walk / k_dict_walk_g, VRec.n_blocks -1 /
-// -2).  Separate kernels, so each is compiled for its own register and LDS
-// budget.
+// 0 = k_dict4, 3 = k_dict4_big.  Separate kernels, so each is compiled for
+// its own register and LDS budget.
 __device__ __forceinline__ void dict_fill0(const VRec& r, int lane, int& de) {
   // a zero-width decoder yields key 0 forever, reading nothing (hybrid_decoder.go:84-86)
   if (r.dcount < 1) de = kDICT_INDEX;
@@ -401,17 +440,6 @@ __device__ __forceinline__ void dict_fill0(const VRec& r, int lane, int& de) {
     const uint32_t d0 = *(const PQG_G uint32_t*)gconst(r.dict);
     for (int64_t i = lane; i < r.nn; i += 64) ((PQG_G uint32_t*)gmut(r.out))[i] = d0;
   }
-}
-
-template <class Dict>
-__device__ __forceinline__ int walk_dict_page(VRec& r, WalkShared& ws, const Dict& dict) {
-  IdxWalk<Dict> iw{gconst(r.p), (uint32_t)r.n, r.w, (uint32_t)r.nn, (PQG_G uint32_t*)gmut(r.out), (uint32_t)r.dcount,
-                   dict, &ws, (uint32_t)((uintptr_t)r.p & (kIWin - 1))};
-  iw.run();
-  // keys are checked only among the produced ones: a bad key comes first
-  const int64_t bad = wave_min((int64_t)iw.bad);
-  if (bad < r.nn) return kDICT_INDEX;
-  return iw.produced < (uint32_t)r.nn ? iw.serr : kOK;
 }
 
 template <int kMode>
@@ -439,26 +467,13 @@ __device__ __forceinline__ void dict_items(PageDev* pages, const int* total, int
     // a zero-width page (key 0 for every value, no run table) stays with
     // k_dict4 whatever its dictionary's size: k_dict_plan raises the big-dict
     // stage flag only for pages with index streams
-    const int own = kMode == 0   ? (r.n_blocks >= 0 && !(big && r.w > 0 && big_dict(r)))
-                    : kMode == 3 ? (r.n_blocks >= 0 && r.w > 0 && big_dict(r))
-                    : kMode == 1 ? (r.n_blocks == -1)
-                                 : (r.n_blocks == -2);
+    const int own = kMode == 0 ? (r.n_blocks >= 0 && !(big && r.w > 0 && big_dict(r)))
+                               : (r.n_blocks >= 0 && r.w > 0 && big_dict(r));
     if (!own) r.job = -1;  // another kernel's page
     PQG_DT(t1);
     pf.add(2, t1 - t0);
-    if constexpr (kMode == 2) {
-      __syncthreads();  // sh.item is read
-      if (r.job < 0) continue;
-      int de = kOK;
-      if (r.w == 0) dict_fill0(r, lane, de);
-      else {
-        const PQG_G uint32_t* dsafe = (const PQG_G uint32_t*)(r.dict ? gconst(r.dict) : gconst(r.out));
-        de = walk_dict_page(r, sh.w[wid], GlobalDict{dsafe});
-      }
-      if (lane == 0 && de != kOK) atomicMin(&pages[r.pidx].decode_status, de);
-      continue;
-    } else {
-    // ---- kMode 0 / 1: the dictionaries of the item's pages into LDS, one job
+    {
+    // ---- the dictionaries of the item's pages into LDS, one job
     // at a time (an item holds pages of at most kDWaves jobs); the pages of
     // the job in LDS decode, then the next job's
     if (lane == 0) sh.wjob[wid] = r.job;
@@ -529,9 +544,6 @@ __device__ __forceinline__ void dict_items(PageDev* pages, const int* total, int
         int de = kOK;
         if (r.w == 0) {
           dict_fill0(r, lane, de);
-        } else if constexpr (kMode == 1) {
-          // k_dict_plan gives this kernel only pages whose dictionary fits LDS
-          de = lds ? walk_dict_page(r, sh.w[wid], LdsDict{lds_ptr(sh.dict)}) : kCAPACITY;
         } else if constexpr (kMode == 3) {
           PieceShared& ps = sh.w[wid];
           const PQG_G uint32_t* dg = (const PQG_G uint32_t*)gconst(r.dict);
@@ -585,21 +597,6 @@ k_dict4(PageDev* pages, const int* total, int* queue, const VRec* recs, int big)
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, kBigWaves * 64), amdgpu_waves_per_eu(2)))
 k_dict4_big(PageDev* pages, const int* total, int* queue, const VRec* recs) {
   dict_items<3>(pages, total, queue, recs, 1);
-}
-
-#ifndef PQG_DICT_WALK_WPE
-#define PQG_DICT_WALK_WPE 3
-#endif
-#ifndef PQG_DICT_WALKG_WPE
-#define PQG_DICT_WALKG_WPE 3
-#endif
-__global__ void __attribute__((amdgpu_flat_work_group_size(1, kDWaves * 64), amdgpu_waves_per_eu(PQG_DICT_WALK_WPE)))
-k_dict_walk(PageDev* pages, const int* total, int* queue, const VRec* recs) {
-  dict_items<1>(pages, total, queue, recs);
-}
-__global__ void __attribute__((amdgpu_flat_work_group_size(1, kDWaves * 64), amdgpu_waves_per_eu(PQG_DICT_WALKG_WPE)))
-k_dict_walk_g(PageDev* pages, const int* total, int* queue, const VRec* recs) {
-  dict_items<2>(pages, total, queue, recs);
 }
 
 }  // namespace pqg

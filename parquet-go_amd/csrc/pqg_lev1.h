@@ -52,26 +52,23 @@ struct L1Hdr {
 // >= 2 are `bad` (the exact decoder settles them).
 // lo / hi: stream bytes q..q+3 / q+4..q+7.
 __device__ __forceinline__ L1Hdr l1_hdr(uint32_t lo, uint32_t hi, uint32_t q, uint32_t n) {
+  // branch-free (every position of a segment is parsed: divergent bit-packed
+  // / RLE branches would run both sides)
   const uint32_t cont = ~lo & 0x80808080u;
-  const uint32_t hl = cont ? (uint32_t)(__builtin_ctz(cont) >> 3) + 1 : 5u;
-  uint32_t h = (lo & 0x7f) | ((lo >> 1) & 0x3f80) | ((lo >> 2) & 0x1fc000) | ((lo >> 3) & 0xfe00000);
-  h &= hl >= 4 ? 0xfffffffu : ((1u << (7 * hl)) - 1);
+  const uint32_t hl = (cont ? (uint32_t)__builtin_ctz(cont) >> 3 : 4u) + 1;  // 5: no terminating byte in four
+  const uint32_t hf = (lo & 0x7f) | ((lo >> 1) & 0x3f80) | ((lo >> 2) & 0x1fc000) | ((lo >> 3) & 0xfe00000);
+  const uint32_t h = __builtin_amdgcn_ubfe(hf, 0, 7 * hl);  // hl 5: garbage, and bad below
   const uint32_t g = h >> 1;
+  const bool bp = (h & 1) != 0;
+  const uint32_t vb = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * hl)) & 0xff;  // the byte after the header
+  const uint32_t ve = q + hl;
   L1Hdr r;
-  r.bp = (h & 1) != 0;
-  r.bad = hl > 4 || q + hl > n || g == 0;
-  if (r.bp) {
-    r.cnt = g * 8;  // g < 2^27
-    r.pay = q + hl;
-    r.nx = q + hl + g;
-  } else {
-    const uint32_t vp = q + hl;
-    const uint32_t v = (hl < 4 ? (lo >> (8 * hl)) : hi) & 0xff;
-    r.bad |= vp >= n || v > 1;  // readRLERunValue: value < 2^w (:127-129)
-    r.cnt = g;
-    r.pay = v;
-    r.nx = vp + 1;
-  }
+  r.bp = bp;
+  // readRLERunValue: the value byte must be there and < 2^w (:116-131)
+  r.bad = (hl > 4) | (ve > n) | (g == 0) | (!bp & ((ve >= n) | (vb > 1)));  // bitwise: no branches
+  r.cnt = bp ? g * 8 : g;  // g < 2^27
+  r.pay = bp ? ve : vb;
+  r.nx = ve + (bp ? g : 1u);
   return r;
 }
 __device__ __forceinline__ L1Hdr l1_parse(const PQG_L uint8_t* win, uint32_t mis, uint32_t q, uint32_t n) {
@@ -81,9 +78,33 @@ __device__ __forceinline__ L1Hdr l1_parse(const PQG_L uint8_t* win, uint32_t mis
   const uint32_t sft = (wo & 3) * 8;
   return l1_hdr(__builtin_amdgcn_alignbit(b, a, sft), __builtin_amdgcn_alignbit(c, b, sft), q, n);
 }
+// A header on the chain (checked by the table walk: <= 4 bytes, no error):
+// the fields the value walks need, without the checks.
+struct L1Run {
+  uint32_t hl, g, vb;  // header bytes, h >> 1, the byte after the header
+  bool bp;
+};
+__device__ __forceinline__ L1Run l1_run(const PQG_L uint8_t* win, uint32_t mis, uint32_t q) {
+  const uint32_t wo = mis + q;
+  const PQG_L uint32_t* d = (const PQG_L uint32_t*)(win + (wo & ~3u));
+  const uint32_t a = d[0], b = d[1], c = d[2];
+  const uint32_t sft = (wo & 3) * 8;
+  const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sft), hi = __builtin_amdgcn_alignbit(c, b, sft);
+  const uint32_t cont = ~lo & 0x80808080u;
+  L1Run r;
+  r.hl = (cont ? (uint32_t)__builtin_ctz(cont) >> 3 : 3u) + 1;
+  const uint32_t hf = (lo & 0x7f) | ((lo >> 1) & 0x3f80) | ((lo >> 2) & 0x1fc000) | ((lo >> 3) & 0xfe00000);
+  const uint32_t h = __builtin_amdgcn_ubfe(hf, 0, 7 * r.hl);
+  r.g = h >> 1;
+  r.bp = (h & 1) != 0;
+  r.vb = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * r.hl)) & 0xff;
+  return r;
+}
+
 // the exit code of a header whose successor lies at or past the segment's end e
 __device__ __forceinline__ uint32_t l1_code(const L1Hdr& h, uint32_t e) {
-  return h.bad ? kL1Bad : (h.nx - e < kL1Far ? h.nx - e : kL1Far);
+  const uint32_t d = h.nx - e;
+  return h.bad ? kL1Bad : (d < kL1Far ? d : kL1Far);
 }
 
 // OR the bits of values [s, s + len) of one run into the bitmap: bit-packed
@@ -167,27 +188,20 @@ __device__ __forceinline__ bool lev1_page(gcu8 p, uint32_t n, uint32_t count, gu
       const uint32_t x0 = up ? d1 : d0, x1 = up ? d2 : d1, x2 = up ? d3 : d2;
       h[j] = l1_hdr(__builtin_amdgcn_alignbit(x1, x0, sft), __builtin_amdgcn_alignbit(x2, x1, sft), q0 + j, n);
     }
-    uint32_t t[4];
+    uint32_t t[4], c[4];
+    bool in[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const bool in = !h[j].bad && h[j].nx < e;
-      t[j] = T[in ? h[j].nx : q0 + 3];  // unconditional (clamped) read
+      in[j] = !h[j].bad & (h[j].nx < e);
+      t[j] = T[in[j] ? h[j].nx : q0 + 3];  // unconditional (clamped) read
+      c[j] = l1_code(h[j], e);
     }
-    uint32_t c3 = l1_code(h[3], e), c2 = l1_code(h[2], e);
-    if (!h[3].bad && h[3].nx < e) c3 = t[3];
-    if (!h[2].bad && h[2].nx < e) c2 = h[2].nx == q0 + 3 ? c3 : t[2];  // never q0 + 3: >= 2 apart
-    uint32_t c1 = l1_code(h[1], e), c0 = l1_code(h[0], e);
-    if (!h[1].bad && h[1].nx < e) c1 = h[1].nx == q0 + 3 ? c3 : t[1];
-    if (!h[0].bad && h[0].nx < e) c0 = h[0].nx == q0 + 3 ? c3 : h[0].nx == q0 + 2 ? c2 : t[0];
-    const uint32_t packed = c0 | c1 << 8 | c2 << 16 | c3 << 24;
-    if ((q0 & 3) == 0) {
-      *(PQG_L uint32_t*)(T + q0) = packed;
-    } else {
-      T[q0] = (uint8_t)c0;
-      T[q0 + 1] = (uint8_t)c1;
-      T[q0 + 2] = (uint8_t)c2;
-      T[q0 + 3] = (uint8_t)c3;
-    }
+    // successors inside the group come from registers (q0 + 2 / q0 + 3: written below)
+    const uint32_t c3 = in[3] ? t[3] : c[3];
+    const uint32_t c2 = in[2] ? t[2] : c[2];  // successor >= q0 + 4
+    const uint32_t c1 = in[1] ? (h[1].nx == q0 + 3 ? c3 : t[1]) : c[1];
+    const uint32_t c0 = in[0] ? (h[0].nx == q0 + 3 ? c3 : h[0].nx == q0 + 2 ? c2 : t[0]) : c[0];
+    *(PQG_L uint32_t*)(T + q0) = c0 | c1 << 8 | c2 << 16 | c3 << 24;  // q0 = a + 4k: aligned
   }
   __builtin_amdgcn_wave_barrier();
   PQG_T(t2);
@@ -219,14 +233,19 @@ __device__ __forceinline__ bool lev1_page(gcu8 p, uint32_t n, uint32_t count, gu
   PQG_T(t3);
   PQG_ACC(22, t2, t3);
   if (!ok) { PQG_ACC(27, 0, 1); return false; }
+#ifdef PQG_L1_STOP_AFTER_LINK  // timing experiment only (wrong outputs)
+  *nn_out = 0;
+  return true;
+#endif
   // ---- 3a. values per segment and the segment's chain positions (bit q - a)
   uint32_t C = 0;
   uint64_t cm = 0;
   for (uint32_t q = myE; q < e;) {
-    const L1Hdr h = l1_parse(win, mis, q, n);
-    C = C + h.cnt < (1u << 24) ? C + h.cnt : (1u << 24);  // > any page count: the scan cannot wrap
+    const L1Run r = l1_run(win, mis, q);
+    const uint32_t cnt = r.bp ? r.g * 8 : r.g;
+    C = C + cnt < (1u << 24) ? C + cnt : (1u << 24);  // > any page count: the scan cannot wrap
     cm |= 1ull << (q - a);
-    q = h.nx;
+    q += r.hl + (r.bp ? r.g : 1u);
   }
   const uint32_t incl = ldpp_incl_add_sat(C);
   const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -255,21 +274,27 @@ __device__ __forceinline__ bool lev1_page(gcu8 p, uint32_t n, uint32_t count, gu
   const uint32_t kfirst = k;
   uint32_t nn = 0;
   uint64_t m = c < count ? cm : 0ull;
+#ifdef PQG_L1_SKIP_EMIT  // timing experiment only (wrong outputs)
+  m = 0;
+#endif
   while (m) {
     const uint32_t q = a + (uint32_t)__builtin_ctzll(m);
     m &= m - 1;
-    const L1Hdr h = l1_parse(win, mis, q, n);
-    uint32_t take = h.cnt < count - c ? h.cnt : count - c;
+    const L1Run r = l1_run(win, mis, q);
+    const uint32_t cnt = r.bp ? r.g * 8 : r.g;
+    uint32_t take = cnt < count - c ? cnt : count - c;
+    const uint32_t pay = q + r.hl;  // bit-packed payload
     // a short read: the last needed group must start inside the stream (Q5)
-    if (h.bp && h.pay + ((take + 7) >> 3) - 1 >= n) { fail = true; break; }
+    if (r.bp && pay + ((take + 7) >> 3) - 1 >= n) { fail = true; break; }
     c += take;
-    const uint32_t pat = h.pay ? 0xffffffffu : 0u;  // RLE
-    uint32_t sb = h.bp ? (mis + h.pay) * 8 : 0u;
+    const uint32_t pat = r.vb ? 0xffffffffu : 0u;  // RLE
+    const bool bp = r.bp;
+    uint32_t sb = bp ? (mis + pay) * 8 : 0u;
     while (take) {
       const uint32_t room = 32 - fill;
       const uint32_t nb = take < room ? take : room;
       const uint32_t src = __builtin_amdgcn_alignbit(W[(sb >> 5) + 1], W[sb >> 5], sb & 31);
-      const uint32_t chunk = (h.bp ? src : pat) & (nb >= 32 ? 0xffffffffu : ((1u << nb) - 1));
+      const uint32_t chunk = (bp ? src : pat) & (nb >= 32 ? 0xffffffffu : ((1u << nb) - 1));
       acc |= chunk << fill;
       fill += nb;
       take -= nb;
@@ -296,7 +321,11 @@ __device__ __forceinline__ bool lev1_page(gcu8 p, uint32_t n, uint32_t count, gu
   // ---- 4. level bytes, 16 per lane per step (whole granules: one aligned
   // 1 KiB wave store per step), the ragged first / last granule bytewise
   const PQG_L uint16_t* B16 = (const PQG_L uint16_t*)lds_ptr(sh.tab);
+#ifdef PQG_L1_SKIP_EXPAND  // timing experiment only (wrong outputs)
+  const uint32_t g0 = 1, g1 = 0;
+#else
   const uint32_t g0 = (pre + 15) >> 4, g1 = end >> 4;  // whole granules [g0, g1)
+#endif
   for (uint32_t g = g0 + (uint32_t)lane; g < g1; g += 64) {
     const uint32_t b16 = B16[g];
     uint32_t wv[4];

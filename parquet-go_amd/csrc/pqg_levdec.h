@@ -1,7 +1,6 @@
 // pqg_levdec.h — the wave-parallel RLE / bit-packed level decoder
-// (LevelDecoder) and the read phase of a data page (page_setup), shared by
-// k_page_levels (pqg_levels.hip) and the fused level + dictionary page kernel
-// (pqg_fused.hip).
+// (LevelDecoder) and the read phase of a data page (page_setup), used by
+// k_page_levels and k_page_levels_w1 (pqg_levels.hip).
 #pragma once
 #include "pqg_common.h"
 #include "pqg_device.h"
@@ -702,11 +701,9 @@ struct PageStreams {
   int64_t val_n;
   int vmode;             // the page's values stage (PageDev.vmode)
 };
-// fused: the caller (k_page_fused) decodes small 4-byte dictionary pages
-// itself and raises the dictionary stage's flag only for the ones it leaves.
 __device__ __forceinline__ PageStreams page_setup(const JobDev& job, const PageDev& pg, int pidx, PageDev* pages,
                                                   HStream* streams, const int* total, const uint8_t* scratch,
-                                                  bool writer, bool fused = false) {
+                                                  bool writer) {
   PageStreams r{nullptr, nullptr, -1, -1, kOK, nullptr, 0, -1};
   gcu8 block;
   int64_t blen;
@@ -788,7 +785,7 @@ __device__ __forceinline__ PageStreams page_setup(const JobDev& job, const PageD
     const int vm = r.vmode;
     P.vmode = vm;
     int* present = const_cast<int*>(total) + kModePresentOff;
-    if (present[vm] == 0 && !(fused && vm == 1)) present[vm] = 1;
+    if (present[vm] == 0) present[vm] = 1;
     // flag 4: DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY pages (k_str_delta, k_str_dba)
     if (vm == 2 && (pg.encoding == 6 || pg.encoding == 7) && present[4] == 0) present[4] = 1;
   }

@@ -118,7 +118,7 @@ __device__ __forceinline__ void sync_ensure(LaneWin& w, bool reads, uint32_t rp)
 // [2 total, 3 total) the value streams, so a wave's lanes do alike work.
 __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pages, const int* list, const int* total,
                                                               HStream* streams, RunEnt* runs, BlockDesc* blks,
-                                                              LongWalk* longs, int long_cap, int skip_dict_small) {
+                                                              LongWalk* longs, int long_cap) {
   static_assert(kWalkThreads == 64, "LaneWin: dword k of lane L at buf[64 k + L]");
   __shared__ uint32_t buf[4 * kLaneWinG * kWalkThreads];  // each lane's 128-byte window (LaneWin)
   const int nt = *total;
@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_hybrid_walk(const PageDev* pag
   for (int g = blockIdx.x * kWalkThreads + threadIdx.x; g < nt; g += gridDim.x * kWalkThreads) {
     const PageDev& pg = pages[list[g]];
     const int hs = pg.hs_val;
-    if (hs < 0 || (skip_dict_small && dict_walk_page(pg))) continue;  // k_dict4 walks those (IdxWalk)
+    if (hs < 0) continue;
     HStream& S = streams[hs];
     const uint32_t w = (uint32_t)S.w;
     const uint32_t n = (uint32_t)S.n, count = (uint32_t)S.count;
@@ -514,8 +514,7 @@ __device__ void plan_parts(JobDev& job, int np, bool fail, const PageDev* pp, co
 // type.  The dictionary is published only when the page's read phase
 // succeeds: the gather sinks bound keys by dict_count alone, so a short page
 // must never be visible (the reference fails the chunk in readPages first).
-// Thread 0 of k_dict_resolve, before the level decode (the fused page kernel
-// gathers from it), after the decompression stages (the page's read status is
+// Thread 0 of k_dict_resolve, before the level decode, after the decompression stages (the page's read status is
 // final then).
 __device__ void resolve_dictionary(JobDev& job, PageDev* pages, uint8_t* scratch) {
   int np = job.num_pages < job.page_cap ? job.num_pages : job.page_cap;

@@ -39,8 +39,6 @@ __global__ void k_cand_link(JobDev* jobs, const int* tile_job, int64_t total_til
                             int* ok2slot);
 __global__ void k_page_chain(JobDev* jobs, PageDev* pages, const Cand* cands, const int* succ,
                              const int* idx2slot, const int* ok2slot, int* order);
-__global__ void k_walk_wave(const PageDev* pages, const int* list, const int* total, int* queue, HStream* streams,
-                            RunEnt* runs, BlockDesc* blks, int skip_dict_small);
 __global__ void k_scan_pages(JobDev* jobs, PageDev* pages, int n_jobs, int prewalk, int stride);
 __global__ void k_page_list(JobDev* jobs, PageDev* pages, int n_jobs, int* list, int list_cap, int* total,
                             int* queues);
@@ -63,13 +61,10 @@ __global__ void k_page_levels_w1(JobDev* jobs, PageDev* pages, const int* list, 
                               uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena,
                               LongLev* longs, int long_cap, LevPiece* pieces, int piece_cap, int split);
 __global__ void k_dict_resolve(JobDev* jobs, int n_jobs, PageDev* pages, uint8_t* scratch);
-__global__ void k_page_fused(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
-                             uint8_t* scratch, HStream* streams, uint8_t* def_arena, uint8_t* rep_arena, LongLev* longs,
-                             int long_cap, LevPiece* pieces, int piece_cap, uint8_t* value_arena, uint64_t* lb);
 __global__ void k_level_long(PageDev* pages, const int* ctr, const LongLev* longs, int long_cap,
                              const LevPiece* pieces, int piece_cap, int* queue);
 __global__ void k_hybrid_walk(const PageDev* pages, const int* list, const int* total, HStream* streams,
-                              RunEnt* runs, BlockDesc* blks, LongWalk* longs, int long_cap, int skip_dict_small);
+                              RunEnt* runs, BlockDesc* blks, LongWalk* longs, int long_cap);
 __global__ void k_walk_long(const int* ctr, const LongWalk* longs, int long_cap, BlockDesc* blks);
 __global__ void k_nn_scan(JobDev* jobs, PageDev* pages, uint8_t* scratch, const HStream* streams, const BlockDesc* blks,
                           int* ctr, PartRec* parts, int64_t parts_cap);
@@ -78,12 +73,10 @@ __global__ void k_values(JobDev* jobs, PageDev* pages, const PartRec* parts, con
                          uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks);
 __global__ void k_dict_plan(JobDev* jobs, PageDev* pages, const PartRec* parts, const int* total,
                             uint8_t* value_arena, const HStream* streams, const RunEnt* runs, const BlockDesc* blks,
-                            VRec* recs, int walk_small);
+                            VRec* recs);
 __global__ void k_dict4(PageDev* pages, const int* total, int* queue, const VRec* recs, int big);
 __global__ void k_dict4_big(PageDev* pages, const int* total, int* queue, const VRec* recs);
 constexpr int kBigDictThreads = 512;
-__global__ void k_dict_walk(PageDev* pages, const int* total, int* queue, const VRec* recs);
-__global__ void k_dict_walk_g(PageDev* pages, const int* total, int* queue, const VRec* recs);
 __global__ void k_finalize(JobDev* jobs, int n_jobs, PageDev* pages);
 __global__ void k_str_dict(JobDev* jobs, PageDev* pages, int64_t* doffs_arena);
 __global__ void k_str_count(JobDev* jobs, PageDev* pages, PartRec* parts, const int* total, int* queue,
@@ -183,23 +176,14 @@ struct pqg_ctx {
   int num_cus = 256;
   DevBuf vrecs;          // VRec per page-list entry (k_dict_plan -> k_dict4)
   int dict4_per_cu = 2;  // resident k_dict4 workgroups per CU (LDS-bound), from the occupancy query
-  int dict_walk_per_cu = 2;  // the same for k_dict_walk
-  int dict_walkg_per_cu = 2; // and k_dict_walk_g
-  int fused_per_cu = 12;     // resident k_page_fused waves per CU (one-wave blocks), from the occupancy query
   int dict4_threads = 256;
   bool dict4 = true;     // k_dict4 for 4-byte dictionary pages (PQG_DICT4=0: k_values<1>, for A/B runs)
-  // Measured alternatives, off by default (C2 on one MI355X, r05_s8: run tables
-  // 3.15 ms/step, in-kernel walk 3.33, fused 3.86):
-  bool walk_wave = false; // PQG_WALK_WAVE=1: k_walk_wave (one wave per value stream) for the run tables
   bool stride = true;     // the K1 stride walk of equal-page chunks (PQG_STRIDE=0: the candidate scan takes them)
   bool dict_big = true;   // k_dict4_big for dictionaries past 4096 entries (PQG_DICT_BIG=0: k_dict4 gathers them)
-  bool dict_walk = false; // PQG_DICT_WALK=1: k_dict_walk / k_dict_walk_g walk small pages' index streams themselves
   bool lev1 = true;       // the whole-page 1-bit level decoder in k_page_levels_w1 (PQG_LEV1=0: the batch decoder alone)
-  bool fused = false;     // PQG_FUSED=1: k_page_fused, levels + small 4-byte dictionary pages in one pass
   int seg_waves = 31;     // PQG_SEG_WAVES: k_snap_seg waves per CU (its 5 KiB of LDS allow 31; 16: C4 +10 %)
   int levlong_waves = 28; // PQG_LEVLONG_WAVES: k_level_long waves per CU (66 VGPRs: 7 per SIMD; 8: C5 0.61 ms, 28: 0.32)
   int link_waves = 16;    // PQG_LINK_WAVES: k_snap_link waves per CU (one wave per big page; 4: C4 +50 %)
-  DevBuf lookback;       // k_page_fused: one look-back word per page
   int snappy_per_cu = 2;  // resident k_snappy waves per CU (LDS-bound: the output history ring)
   DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
   DevBuf tile_job;  // K1: tile -> job
@@ -237,6 +221,7 @@ struct pqg_ctx {
   hipEvent_t ev_k8[4];   // K8: [0,1] assemble / list count, [2,3] list write
   float k8_ms = 0.f;     // device time of the last pqg_assemble / pqg_assemble_list
   bool timed = true;
+  bool last_timed = false;              // the last pipeline launch recorded the stage events
 };
 
 static int hip_ok(hipError_t e) { return e == hipSuccess ? PQG_OK : PQG_ERR_HIP; }
@@ -286,11 +271,8 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
   for (auto& e : c->ev) hipEventCreate(&e);
   for (auto& e : c->ev_k8) hipEventCreate(&e);
   if (const char* e = getenv("PQG_DICT4")) c->dict4 = atoi(e) != 0;
-  if (const char* e = getenv("PQG_DICT_WALK")) c->dict_walk = atoi(e) != 0;
   if (const char* e = getenv("PQG_DICT_BIG")) c->dict_big = atoi(e) != 0;
   if (const char* e = getenv("PQG_STRIDE")) c->stride = atoi(e) != 0;
-  if (const char* e = getenv("PQG_WALK_WAVE")) c->walk_wave = atoi(e) != 0;
-  if (const char* e = getenv("PQG_FUSED")) c->fused = atoi(e) != 0;
   if (const char* e = getenv("PQG_LEV1")) c->lev1 = atoi(e) != 0;
   if (const char* e = getenv("PQG_SEG_WAVES")) c->seg_waves = atoi(e) > 0 ? atoi(e) : c->seg_waves;
   if (const char* e = getenv("PQG_LEVLONG_WAVES")) c->levlong_waves = atoi(e) > 0 ? atoi(e) : c->levlong_waves;
@@ -303,18 +285,6 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, reinterpret_cast<const void*>(&k_dict4), c->dict4_threads, 0) ==
             hipSuccess && o > 0)
       c->dict4_per_cu = o;
-    o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, reinterpret_cast<const void*>(&k_dict_walk), c->dict4_threads, 0) ==
-            hipSuccess && o > 0)
-      c->dict_walk_per_cu = o;
-    o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, reinterpret_cast<const void*>(&k_dict_walk_g), c->dict4_threads, 0) ==
-            hipSuccess && o > 0)
-      c->dict_walkg_per_cu = o;
-    o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, reinterpret_cast<const void*>(&k_page_fused), 64, 0) ==
-            hipSuccess && o > 0)
-      c->fused_per_cu = o;
   }
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&k_snappy), 64, 0) ==
@@ -341,7 +311,7 @@ void pqg_ctx_destroy(pqg_ctx* c) {
                     &c->ok2slot, &c->order, &c->asm_seg, &c->offs_arena, &c->doffs_arena, &c->page_stage,
                     &c->blk_src, &c->blk_dst, &c->blk_meta, &c->tile_job, &c->sn_subs, &c->sn_segpage, &c->sn_F,
                     &c->blk_subs, &c->blk_segpage, &c->blk_F, &c->vrecs, &c->parts, &c->lev_long, &c->lev_pieces,
-                    &c->walk_long, &c->lookback})
+                    &c->walk_long})
     b->release();
   if (c->h_jobs) hipHostFree(c->h_jobs);
   hipStreamDestroy(c->stream);
@@ -502,7 +472,6 @@ static int plan_batch(pqg_ctx* c) {
       c->runs.grow(sizeof(RunEnt) * (size_t)run_total + 8192) || c->blks.grow(sizeof(BlockDesc) * (size_t)blk_total + 8192) ||
       c->vrecs.grow(sizeof(VRec) * (size_t)std::max<int64_t>(c->parts_cap, 1)) ||
       c->offs_arena.grow(sizeof(int64_t) * (size_t)offs_total + 64) ||
-      c->lookback.grow(sizeof(uint64_t) * (size_t)std::max<int64_t>(page_total, 1)) ||
       c->doffs_arena.grow(sizeof(int64_t) * (size_t)doffs_total + 64))
     return PQG_ERR_HIP;
   c->total_tiles = tile_total;
@@ -537,6 +506,7 @@ static void launch_snappy(pqg_ctx* c, hipStream_t s, JobDev* jobs, PageDev* page
 static int launch_pipeline(pqg_ctx* c) {
   const int n = c->n_jobs;
   c->launches++;
+  c->last_timed = c->timed;
   JobDev* jobs = (JobDev*)c->jobs.p;
   PageDev* pages = (PageDev*)c->pages.p;
   int* list = (int*)c->list.p;
@@ -607,32 +577,24 @@ static int launch_pipeline(pqg_ctx* c) {
   LongLev* llong = (LongLev*)c->lev_long.p;
   LevPiece* lpieces = (LevPiece*)c->lev_pieces.p;
   const int llc = (int)std::min<int64_t>(c->lev_long_cap, INT32_MAX), lpc = (int)std::min<int64_t>(c->lev_piece_cap, INT32_MAX);
-  // each job's dictionary page (the fused kernel gathers from it)
+  // each job's dictionary page
   hipLaunchKernelGGL(k_dict_resolve, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, jobs, n, pages, scratch);
-  const bool fused = c->fused && c->dict4 && c->dict_walk;
-  if (fused) {  // levels + the small 4-byte dictionary pages' values (pqg_fused.hip)
-    hipMemsetAsync(c->lookback.p, 0, sizeof(uint64_t) * (size_t)std::max<int64_t>(c->list_cap, 1), s);
-    hipLaunchKernelGGL(k_page_fused, dim3((unsigned)(c->num_cus * c->fused_per_cu)), dim3(64), 0, s, jobs, pages, list,
-                       ctr, Q(1), scratch, streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p, llong, llc,
-                       lpieces, lpc, (uint8_t*)c->value_arena.p, (uint64_t*)c->lookback.p);
-  } else {
-    // pages of jobs with 1-bit levels (maxR = 0, maxD <= 1) to the w = 1
-    // decoder, the others to the general one; a kernel with no job stays idle
-    bool any_w1 = false, any_gen = false;
-    for (int i = 0; i < n; i++) {
-      const pqg_column_desc& d = c->cur[(size_t)i].col;
-      (d.max_rep == 0 && d.max_def <= 1 ? any_w1 : any_gen) = true;
-    }
-    const int split = any_w1 && any_gen;
-    if (any_w1)
-      hipLaunchKernelGGL(k_page_levels_w1, dim3(qgrid(c->num_cus * 32)), dim3(64), 0, s, jobs, pages, list, ctr, Q(1),
-                         scratch, streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p, llong, llc, lpieces, lpc,
-                         split | (c->lev1 ? 2 : 0));
-    if (any_gen)
-      hipLaunchKernelGGL(k_page_levels, dim3(qgrid(c->num_cus * 24)), dim3(64), 0, s, jobs, pages, list, ctr,
-                         Q(split ? kQueueLevGen : 1), scratch, streams, (uint8_t*)c->def_arena.p,
-                         (uint8_t*)c->rep_arena.p, llong, llc, lpieces, lpc, split);
+  // pages of jobs with 1-bit levels (maxR = 0, maxD <= 1) to the w = 1
+  // decoder, the others to the general one; a kernel with no job stays idle
+  bool any_w1 = false, any_gen = false;
+  for (int i = 0; i < n; i++) {
+    const pqg_column_desc& d = c->cur[(size_t)i].col;
+    (d.max_rep == 0 && d.max_def <= 1 ? any_w1 : any_gen) = true;
   }
+  const int split = any_w1 && any_gen;
+  if (any_w1)
+    hipLaunchKernelGGL(k_page_levels_w1, dim3(qgrid(c->num_cus * 32)), dim3(64), 0, s, jobs, pages, list, ctr, Q(1),
+                       scratch, streams, (uint8_t*)c->def_arena.p, (uint8_t*)c->rep_arena.p, llong, llc, lpieces, lpc,
+                       split | (c->lev1 ? 2 : 0));
+  if (any_gen)
+    hipLaunchKernelGGL(k_page_levels, dim3(qgrid(c->num_cus * 24)), dim3(64), 0, s, jobs, pages, list, ctr,
+                       Q(split ? kQueueLevGen : 1), scratch, streams, (uint8_t*)c->def_arena.p,
+                       (uint8_t*)c->rep_arena.p, llong, llc, lpieces, lpc, split);
   // stages with no possible work are not launched (the host knows each job's
   // type and levels; the kernels' own flags stay as the backstop)
   if (c->any_levels)
@@ -643,15 +605,10 @@ static int launch_pipeline(pqg_ctx* c) {
       1, std::min<int64_t>((c->list_cap + kWalkLanes - 1) / kWalkLanes, c->num_cus * (2048 / kWalkLanes)));
   LongWalk* wlong = (LongWalk*)c->walk_long.p;
   const int wlc = (int)std::min<int64_t>(c->walk_long_cap, INT32_MAX);
-  const int walk_small = c->dict4 && c->dict_walk;  // small 4-byte dictionary pages: walked in k_dict4
-  if (c->walk_wave) {  // one wave per value stream (pqg_tablewalk.hip)
-    hipLaunchKernelGGL(k_walk_wave, dim3(qgrid(c->num_cus * 20)), dim3(64), 0, s, pages, list, ctr, Q(kQueueWalkWave),
-                       streams, runs, blks, walk_small);
-  } else {  // one lane per value stream
-    hipLaunchKernelGGL(k_hybrid_walk, dim3(walk_blocks), dim3(kWalkLanes), 0, s, pages, list, ctr, streams, runs, blks,
-                       wlong, wlc, walk_small);
-    hipLaunchKernelGGL(k_walk_long, dim3(c->num_cus * 2), dim3(256), 0, s, ctr, wlong, wlc, blks);
-  }
+  // one lane per value stream
+  hipLaunchKernelGGL(k_hybrid_walk, dim3(walk_blocks), dim3(kWalkLanes), 0, s, pages, list, ctr, streams, runs, blks,
+                     wlong, wlc);
+  hipLaunchKernelGGL(k_walk_long, dim3(c->num_cus * 2), dim3(256), 0, s, ctr, wlong, wlc, blks);
   if (c->timed) hipEventRecord(c->ev[5], s);
   if (c->timed) hipEventRecord(c->ev[6], s);
   PartRec* parts = (PartRec*)c->parts.p;
@@ -665,8 +622,7 @@ static int launch_pipeline(pqg_ctx* c) {
   } else if (c->dict4) {  // 4-byte dictionary pages: pieces staged in LDS, small dictionaries in LDS (pqg_dict.hip)
     VRec* recs = (VRec*)c->vrecs.p;
     hipLaunchKernelGGL(k_dict_plan, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((items_cap + 255) / 256, c->num_cus * 4))),
-                       dim3(256), 0, s, jobs, pages, parts, ctr, (uint8_t*)c->value_arena.p, streams, runs, blks, recs,
-                       walk_small);
+                       dim3(256), 0, s, jobs, pages, parts, ctr, (uint8_t*)c->value_arena.p, streams, runs, blks, recs);
     // dictionaries past 4096 entries: k_dict4_big (a 104 KiB LDS prefix, one
     // 8-wave workgroup per CU) takes their run-table pages (PQG_DICT_BIG=0: k_dict4)
     hipLaunchKernelGGL(k_dict4, dim3(qgrid(c->num_cus * c->dict4_per_cu)), dim3(c->dict4_threads), 0, s, pages, ctr, Q(3),
@@ -674,12 +630,6 @@ static int launch_pipeline(pqg_ctx* c) {
     if (c->dict_big)
       hipLaunchKernelGGL(k_dict4_big, dim3(qgrid(c->num_cus)), dim3(kBigDictThreads), 0, s, pages, ctr,
                          Q(kQueueDictBig), recs);
-    if (walk_small) {
-      hipLaunchKernelGGL(k_dict_walk, dim3(qgrid(c->num_cus * c->dict_walk_per_cu)), dim3(c->dict4_threads), 0, s, pages,
-                         ctr, Q(kQueueDictWalk), recs);
-      hipLaunchKernelGGL(k_dict_walk_g, dim3(qgrid(c->num_cus * c->dict_walkg_per_cu)), dim3(c->dict4_threads), 0, s,
-                         pages, ctr, Q(kQueueDictWalkG), recs);
-    }
   } else
     hipLaunchKernelGGL(k_values<1>, dim3(qgrid(waves)), dim3(64), 0, s, jobs, pages, parts, ctr, Q(3),
                        (uint8_t*)c->value_arena.p, streams, runs, blks);
@@ -1146,6 +1096,7 @@ int pqg_set_timing(pqg_ctx* c, int on) {
 
 int pqg_last_timings(pqg_ctx* c, float* out, int cap) {
   if (!c || !out) return PQG_ERR_INVALID_ARG;
+  if (!c->last_timed) return 0;  // the last decode recorded no events: nothing to report
   int k = 0;
   float tot = 0;
   hipEventElapsedTime(&tot, c->ev[0], c->ev[kStages]);

@@ -1031,10 +1031,8 @@ __global__ void __launch_bounds__(1024) k_page_list(JobDev* jobs, PageDev* pages
     if (i < n && (cur.type == 0 || cur.type == 3)) {
       const int64_t B = cur.so >= 0 ? (int64_t)(uint32_t)cur.usize : (int64_t)(uint32_t)cur.csize;
       nr = B / 2 + 2;
-      // the lane walker's greedy blocks need n/kHBlock + runs/kHBlockRuns +
-      // B/(kHBlockBytes/2) + 3; the wave walker's merged batches up to twice
-      // the first two terms (pqg_tablewalk.hip)
-      nb = 2 * (int64_t)(uint32_t)cur.nv / kHBlock + 2 * nr / kHBlockRuns + B / (kHBlockBytes / 2) + 5;
+      // the lane walker's greedy blocks: n/kHBlock + runs/kHBlockRuns + B/(kHBlockBytes/2) + 3
+      nb = (int64_t)(uint32_t)cur.nv / kHBlock + nr / kHBlockRuns + B / (kHBlockBytes / 2) + 3;
     }
     int64_t tr, tb;
     const int64_t er = block_excl_scan<1024>(nr, &tr, part);

@@ -1,6 +1,6 @@
-"""Dictionary index streams of 4-byte dictionary pages on each decode path
-(run tables + k_dict4, the in-kernel walk IdxWalk, the fused level + index
-pass) against the oracle: hand-built dictionary chunks whose RLE_DICTIONARY pages
+"""Dictionary index streams of 4-byte dictionary pages (run tables from
+k_hybrid_walk + k_dict4 / k_dict4_big), with either level decoder, against
+the oracle: hand-built dictionary chunks whose RLE_DICTIONARY pages
 carry index streams with run-level control at every bit width 1..32 -- RLE
 runs of 1 value to far past one batch, bit-packed runs of one group to
 hundreds (payload crossing the ring window), redundant varint header bytes
@@ -73,12 +73,11 @@ def dict_chunk(rng, pages, w, dcount, nullable=True, bad_frac=0.0, short_frac=0.
     return b"".join(parts)
 
 
-# the decode paths of 4-byte dictionary pages (pqg_runtime.hip): run tables
-# from the lane walker + k_dict4 (default), run tables from the wave walker
-# (PQG_WALK_WAVE=1), the in-kernel walk (PQG_DICT_WALK=1) and the fused level
-# + index pass (PQG_FUSED=1); read when the context is created
-PATHS = {"tables": {}, "wave_tables": {"PQG_WALK_WAVE": "1"}, "walk": {"PQG_DICT_WALK": "1"},
-         "fused": {"PQG_DICT_WALK": "1", "PQG_FUSED": "1"}}
+# the decode paths (pqg_runtime.hip, read when the context is created): the
+# default one (run tables from the lane walker + k_dict4, 1-bit levels by the
+# whole-page decoder, pqg_lev1.h) and the same with the batch level decoder
+# alone (PQG_LEV1=0: the fallback of pages the whole-page decoder does not take)
+PATHS = {"default": {}, "batch_levels": {"PQG_LEV1": "0"}}
 
 
 @pytest.fixture(scope="module", params=list(PATHS))
@@ -86,7 +85,7 @@ def dec(request):
     import os
     import pqgpu
     env = PATHS[request.param]
-    old = {k: os.environ.get(k) for k in ("PQG_DICT_WALK", "PQG_FUSED", "PQG_WALK_WAVE")}
+    old = {k: os.environ.get(k) for k in ("PQG_LEV1",)}
     os.environ.update(env)
     try:
         d = pqgpu.GpuDecoder(0)
