@@ -270,49 +270,66 @@ __device__ __forceinline__ bool lev1_page(gcu8 p, uint32_t n, uint32_t count, gu
   const PQG_L uint32_t* W = (const PQG_L uint32_t*)win;
   bool fail = false;
   uint32_t c = B;
-  uint32_t k = (pre + c) >> 5, fill = (pre + c) & 31, acc = 0;
+  uint32_t k = (pre + c) >> 5, fill = (pre + c) & 31;
+  uint64_t acc = 0;  // bits [32 k, 32 k + fill) of the bitmap (a run of <= 32 values is one step)
   const uint32_t kfirst = k;
   uint32_t nn = 0;
   uint64_t m = c < count ? cm : 0ull;
 #ifdef PQG_L1_SKIP_EMIT  // timing experiment only (wrong outputs)
   m = 0;
 #endif
-  while (m) {
-    const uint32_t q = a + (uint32_t)__builtin_ctzll(m);
+  auto flush = [&](uint32_t word) {
+    if (k == kfirst) __hip_atomic_fetch_or(bm + k, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    else bm[k] = word;
+    nn += __builtin_popcount(word);
+    k++;
+  };
+  // the next run's header is read while the current one's bits are placed
+  uint32_t rq = 0;
+  L1Run r{};
+  if (m) {
+    rq = a + (uint32_t)__builtin_ctzll(m);
     m &= m - 1;
-    const L1Run r = l1_run(win, mis, q);
-    const uint32_t cnt = r.bp ? r.g * 8 : r.g;
+    r = l1_run(win, mis, rq);
+  }
+  bool more = c < count && cm != 0;
+  while (more) {
+    const L1Run cur = r;
+    const uint32_t cq = rq;
+    const bool next = m != 0;
+    if (next) {
+      rq = a + (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      r = l1_run(win, mis, rq);
+    }
+    const uint32_t cnt = cur.bp ? cur.g * 8 : cur.g;
     uint32_t take = cnt < count - c ? cnt : count - c;
-    const uint32_t pay = q + r.hl;  // bit-packed payload
+    const uint32_t pay = cq + cur.hl;  // bit-packed payload
     // a short read: the last needed group must start inside the stream (Q5)
-    if (r.bp && pay + ((take + 7) >> 3) - 1 >= n) { fail = true; break; }
+    if (cur.bp && pay + ((take + 7) >> 3) - 1 >= n) { fail = true; break; }
     c += take;
-    const uint32_t pat = r.vb ? 0xffffffffu : 0u;  // RLE
-    const bool bp = r.bp;
+    const uint32_t pat = cur.vb ? 0xffffffffu : 0u;  // RLE
+    const bool bp = cur.bp;
     uint32_t sb = bp ? (mis + pay) * 8 : 0u;
     while (take) {
-      const uint32_t room = 32 - fill;
-      const uint32_t nb = take < room ? take : room;
+      const uint32_t nb = take < 32 ? take : 32;
       const uint32_t src = __builtin_amdgcn_alignbit(W[(sb >> 5) + 1], W[sb >> 5], sb & 31);
-      const uint32_t chunk = (bp ? src : pat) & (nb >= 32 ? 0xffffffffu : ((1u << nb) - 1));
-      acc |= chunk << fill;
+      const uint32_t bits = (bp ? src : pat) & (nb >= 32 ? 0xffffffffu : ((1u << nb) - 1));
+      acc |= (uint64_t)bits << fill;
       fill += nb;
       take -= nb;
       sb += nb;
-      if (fill == 32) {
-        if (k == kfirst) __hip_atomic_fetch_or(bm + k, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        else bm[k] = acc;
-        nn += __builtin_popcount(acc);
-        k++;
-        acc = 0;
-        fill = 0;
+      if (fill >= 32) {
+        flush((uint32_t)acc);
+        acc >>= 32;
+        fill -= 32;
       }
     }
-    if (c >= count) break;
+    more = next && c < count;
   }
   if (fill) {
-    __hip_atomic_fetch_or(bm + k, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    nn += __builtin_popcount(acc);
+    __hip_atomic_fetch_or(bm + k, (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    nn += __builtin_popcount((uint32_t)acc);
   }
   if (__ballot(fail)) return false;
   PQG_T(t5);
