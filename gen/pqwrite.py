@@ -306,9 +306,16 @@ def config_c4(rows=50_000_000, vocab=65536, rows_per_page=20000, seed=4, dict_li
     out_offs[1:] = np.cumsum(lens)
     starts = offs[:-1][ranks]
     total = int(out_offs[-1])
-    # gather chars
-    idx = np.repeat(starts - out_offs[:-1], lens) + np.arange(total, dtype=np.int64)
-    out_chars = chars[idx]
+    # gather chars, 2 M rows at a time (a whole-column index array would be
+    # 8 bytes per char, ~20 GB of host memory at 50 M rows)
+    out_chars = np.empty(total, dtype=np.uint8)
+    step = 1 << 21
+    for r0 in range(0, rows, step):
+        r1 = min(rows, r0 + step)
+        c0, c1 = int(out_offs[r0]), int(out_offs[r1])
+        idx = np.repeat(starts[r0:r1] - out_offs[r0:r1], lens[r0:r1]) + np.arange(c0, c1, dtype=np.int64)
+        out_chars[c0:c1] = chars[idx]
+    del idx
     col = Column("s", BYTE_ARRAY, out_chars, offsets=out_offs, encoding=RLE_DICTIONARY, codec=codec,
                  rows_per_page=rows_per_page, dict_limit=dict_limit)
     return write_file([col], rows), {"rows": rows, "chars": out_chars, "offsets": out_offs}
