@@ -308,7 +308,7 @@ def cpu_baseline(wl, seconds):
 STAGE_KERNELS = {"scan": ["k_scan_pages", "k_tile_jobs", "k_page_cands", "k_cand_parse", "k_tile_scan", "k_cand_link",
                           "k_page_chain"],
                  "list": ["k_page_list"],
-                 "snappy": ["k_snap_plan", "k_snap_seg", "k_snap_link", "k_snap_decode", "k_snappy", "k_inflate"],
+                 "snappy": ["k_snap_plan", "k_snap_seg", "k_snap_link", "k_snap_decode", "k_snappy", "k_inflate_s", "k_inflate"],
                  "levels": ["k_dict_resolve", "k_page_levels", "k_level_long"],
                  "walk": ["k_hybrid_walk", "k_walk_long"], "unused": [], "nn_scan": ["k_nn_scan"],
                  "values": ["k_values", "k_dict_plan", "k_dict4"],
@@ -432,10 +432,10 @@ def run_workload(wl, decs, args, steps, warmup, barrier, dist, world, rank, cpu_
     dom = int(np.argmax(stage_ms))
     dom_name = STAGES[dom]
     achieved = alg[dom_name] / (stage_ms[dom] * 1e-3) / 1e9 if stage_ms[dom] > 0 else 0.0
-    # the decompression stage runs k_inflate for GZIP chunks, the snappy kernels otherwise
+    # the decompression stage runs k_inflate_s (+ k_inflate) for GZIP chunks, the snappy kernels otherwise
     gz = wl.key == "c3_gzip"
     dom_label = ("inflate" if gz else "snappy") if dom_name == "snappy" else dom_name
-    dom_kernels = [k for k in STAGE_KERNELS[dom_name] if dom_name != "snappy" or (k == "k_inflate") == gz]
+    dom_kernels = [k for k in STAGE_KERNELS[dom_name] if dom_name != "snappy" or k.startswith("k_inflate") == gz]
     out = {
         "workload": wl.desc,
         "value": round(b_out * world / elapsed * steps / 1e9, 3),

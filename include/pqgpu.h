@@ -108,9 +108,10 @@ enum {
                                    decoded whole by one wave (its 64 KiB sub-block
                                    split failed: a copy across a 64 KiB block
                                    boundary, or a corrupt block) */
-  PQG_PAGE_FLAG_FUSED = 32        /* libpqgpu diagnostic: the page's levels and
-                                   dictionary keys were decoded in one pass
-                                   (k_page_fused, PQG_FUSED=1; off by default) */
+  PQG_PAGE_FLAG_INFLATE_REDO = 64 /* libpqgpu diagnostic: the page's GZIP stream was
+                                   decoded again with the full 32 KiB window ring
+                                   (a match reached back past the 8 KiB ring to
+                                   bytes past the page's size) */
 };
 
 /* ---- column / chunk description ----------------------------------------- */

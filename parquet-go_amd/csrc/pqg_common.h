@@ -88,6 +88,7 @@ struct PageDev {
   int64_t gz_len;          // K2g (pqg_inflate.hip), bare blocks: decoded bytes
 };
 constexpr int32_t kPageBareBlock = 1 << 4;  // PageDev.flags: a pqg_block_decompress block (no page around it)
+constexpr int32_t kPageInflateRedo = 1 << 6;  // PageDev.flags: a GZIP page for k_inflate's 32 KiB ring (k_inflate_s left it)
 constexpr int32_t kCodecSnappy = 1, kCodecGzip = 2;
 
 // K2 snappy sub-block: the output [j * kSnapSub, (j + 1) * kSnapSub) of one
@@ -300,8 +301,9 @@ constexpr int kQueueLevLong = 13;  // pieces of the long level runs (k_level_lon
 constexpr int kQueueInflate = 14;  // GZIP pages (k_inflate)
 constexpr int kQueueLevGen = 15;  // k_page_levels when k_page_levels_w1 takes the w = 1 jobs' pages
 constexpr int kQueueDictBig = 16; // k_dict4_big: run-table pages of dictionaries past 4096 entries
-// queue regions zeroed per launch: 0-8, the stage flags (9), 10-16
-constexpr int kQueueSlots = 17;
+constexpr int kQueueInflateRedo = 17;  // k_inflate (32 KiB ring) over the pages k_inflate_s left
+// queue regions zeroed per launch: 0-8, the stage flags (9), 10-17
+constexpr int kQueueSlots = 18;
 constexpr int kPresentBigDict = 8;  // stage flag (kModePresentOff + 8): a page for k_dict4_big
 
 // Scan tiles of the speculative page-header search.

@@ -8,7 +8,9 @@
 // classifies them (oracle/pq_oracle.cpp gzip_decode); a decoded length other
 // than the page's uncompressed size is PQG_ERR_SIZE (compress.go:117).
 //
-// One wave per compressed page.  DEFLATE is a serial bit stream, so the
+// One wave per compressed page (k_inflate_s: an 8 KiB history ring, older
+// matches read back from the stored output; k_inflate: the 32 KiB window).
+// DEFLATE is a serial bit stream, so the
 // symbol decode runs wave-uniform (every lane holds the same decoder state;
 // table reads are LDS broadcasts) with canonical-Huffman tables built per
 // block in LDS (a 9-bit fast table, then the count / symbol walk of RFC 1951
@@ -24,11 +26,28 @@
 
 namespace pqg {
 
+#ifdef PQG_PROFILE
+// host reader of this translation unit's counters (pqg_debug_counters 160..191)
+int prof_read_inflate(unsigned long long* out) {
+  unsigned long long z[64] = {0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pqg_prof), sizeof(z)) != hipSuccess) return -1;
+  hipMemcpyToSymbol(HIP_SYMBOL(pqg_prof), z, sizeof(z));
+  return 0;
+}
+#define PQG_CNT(i, v) (f_cnt[i] += (v))
+#else
+#define PQG_CNT(i, v) ((void)0)
+#endif
+
 namespace {
 
 constexpr int kRing = 32768;      // DEFLATE window: the whole history a distance can reach
+#ifndef PQG_INFLATE_RING
+#define PQG_INFLATE_RING 8192
+#endif
+constexpr int kRingSmall = PQG_INFLATE_RING;  // k_inflate_s: older history is read back from the flushed output
 constexpr int kInStage = 1024;    // compressed bytes staged in LDS per refill
-constexpr int kFlush = 16384;     // decoded bytes flushed (and CRC'd) at a time
+constexpr int kInflateRedo = 0x7ffe;  // k_inflate_s: a page for the 32 KiB-ring pass (not a status)
 constexpr int kFastBits = 9;
 constexpr uint32_t kCrcPoly = 0xedb88320u;  // CRC-32 (IEEE, reflected): gzip trailer
 
@@ -38,8 +57,9 @@ struct Huff {
   uint16_t fast[1 << kFastBits];  // next 9 stream bits -> (length << 9) | symbol, 0: longer code
 };
 
+template <int kRingT>
 struct InflateShared {
-  uint8_t ring[kRing];
+  uint8_t ring[kRingT];
   uint8_t in[kInStage + 16];
   uint32_t crc_tab[256];
   uint32_t seg_crc[64];
@@ -48,64 +68,90 @@ struct InflateShared {
   int err;  // table build errors (any lane)
 };
 
-__device__ const uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                          31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__device__ const uint8_t kLenExt[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__device__ const uint16_t kDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
-                                           193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__device__ const uint8_t kDistExt[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+// RFC 1951 3.2.5 length and distance codes, computed (no table loads on the
+// match path): length code s (symbol 257 + s) and distance code ds
+__device__ __forceinline__ uint32_t len_ext(uint32_t s) { return s < 8 || s == 28 ? 0u : (s >> 2) - 1; }
+__device__ __forceinline__ uint32_t len_base(uint32_t s, uint32_t ext) {
+  return s < 8 ? s + 3 : s == 28 ? 258u : ((4 + (s & 3)) << ext) + 3;
+}
+__device__ __forceinline__ uint32_t dist_ext(uint32_t ds) { return ds < 4 ? 0u : (ds >> 1) - 1; }
+__device__ __forceinline__ uint32_t dist_base(uint32_t ds, uint32_t ext) {
+  return ds < 4 ? ds + 1 : ((2 + (ds & 1)) << ext) + 1;
+}
 __device__ const uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// a * b mod P over GF(2), reflected (bit 31 = x^0): zlib's multmodp
-__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
-  uint32_t m = 1u << 31, p = 0;
-  for (;;) {
-    if (a & m) {
-      p ^= b;
-      if ((a & (m - 1)) == 0) break;
-    }
-    m >>= 1;
-    b = b & 1 ? (b >> 1) ^ kCrcPoly : b >> 1;
+// a * b mod P over GF(2), reflected (bit 31 = x^0): zlib's multmodp,
+// branch-free (32 fixed steps: the lanes of a CRC combine hold different a)
+__host__ __device__ constexpr uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll 4
+  for (int i = 0; i < 32; i++) {
+    p ^= b & (0u - ((a >> (31 - i)) & 1u));
+    b = (b >> 1) ^ (kCrcPoly & (0u - (b & 1u)));
   }
   return p;
 }
-// x^(8 n) mod P
+// x^(2^k) mod P, k = 0..31 (zlib's x2n_table; the period is 32)
+struct X2n {
+  uint32_t v[32];
+};
+constexpr X2n make_x2n() {
+  X2n t{};
+  uint32_t p = 1u << 30;  // x^1
+  t.v[0] = p;
+  for (int k = 1; k < 32; k++) t.v[k] = p = multmodp(p, p);
+  return t;
+}
+__device__ const X2n kX2n = make_x2n();
+// x^(8 n) mod P: one multiply per set bit of n (zlib's x2nmodp(n, 3))
 __device__ __forceinline__ uint32_t x8nmodp(uint64_t n) {
-  uint32_t p = 1u << 31;       // x^0
-  uint32_t sq = 1u << 23;      // x^8
-  while (n) {
-    if (n & 1) p = multmodp(sq, p);
-    n >>= 1;
-    sq = multmodp(sq, sq);
-  }
+  uint32_t p = 1u << 31;  // x^0
+  for (int k = 3; n; k++, n >>= 1)
+    if (n & 1) p = multmodp(kX2n.v[k & 31], p);
   return p;
 }
 
 }  // namespace
 
+
 // One wave's inflater.  Every lane holds the same state (wave-uniform control
-// flow); `lane` splits the byte-parallel steps.
+// flow); `lane` splits the byte-parallel steps.  kRingT: the LDS history ring.
+// A ring smaller than the 32 KiB window (k_inflate_s: 8 KiB, so ~10 waves fit
+// a CU instead of 4) flushes every kRingT / 2 decoded bytes, so a match
+// reaching further back than the ring finds its bytes already stored in the
+// page's output: they are read back from there (L2).  Such a byte at or past
+// the output's capacity (a page decoding to more than its size) was never
+// stored: the page goes to the 32 KiB-ring pass (kInflateRedo).
+template <int kRingT, typename Ix>
 struct Inflater {
-  InflateShared* sh;
+  static constexpr int kFlushT = kRingT >= 32768 ? 16384 : kRingT / 2;  // decoded bytes flushed (and CRC'd) at a time
+  static_assert(kFlushT + 258 + 64 <= kRingT, "unflushed bytes and a match must fit the ring");
+  InflateShared<kRingT>* sh;
   gcu8 src;
-  int64_t n;            // compressed bytes
-  int64_t pos = 0;      // next byte for the bit buffer
-  int64_t in_base = -(int64_t)kInStage * 4;  // stream offset of in[0]
+  Ix n;            // compressed bytes
+  Ix pos = 0;      // next byte for the bit buffer
+  Ix in_base = -(Ix)kInStage * 4;  // stream offset of in[0]
   uint64_t bitbuf = 0;
   int bitcnt = 0;
   gu8 dst;              // decoded bytes (cap of them are stored)
-  int64_t cap;
-  int64_t d = 0;        // decoded bytes so far
-  int64_t flushed = 0;  // decoded bytes flushed (stored and CRC'd)
-  int64_t mstart = 0;   // first decoded byte of the current member
+  Ix cap;
+  Ix d = 0;        // decoded bytes so far
+  Ix flushed = 0;  // decoded bytes flushed (stored and CRC'd)
+  Ix mstart = 0;   // first decoded byte of the current member
   uint32_t crc = 0;     // CRC-32 of the member's flushed bytes (conditioned)
   int lane;
+#ifdef PQG_PROFILE
+  // 0 literals, 1 matches, 2 far matches, 3 slow decodes, 4 slow-walk bits,
+  // 5 flush cycles, 6 stage() refills, 7 match bytes
+  uint64_t f_cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 
-  __device__ __forceinline__ void stage(int64_t at) {
+  __device__ __forceinline__ void stage(Ix at) {
     // 16-byte granules from the aligned address at or below `at`; granules
     // past the block re-read its last one (never used)
+    PQG_CNT(6, 1);
     const uintptr_t a0 = (uintptr_t)(src + at) & ~(uintptr_t)15;
-    in_base = at - (int64_t)((uintptr_t)(src + at) - a0);
+    in_base = at - (Ix)((uintptr_t)(src + at) - a0);
     const uintptr_t last = ((uintptr_t)(src + n) - 1) & ~(uintptr_t)15;
     const uintptr_t a = a0 + 16 * (uintptr_t)lane;
     const uint4 v = ldg16(a <= last ? a : last);
@@ -113,16 +159,16 @@ struct Inflater {
     sts16(lds_ptr(sh->in) + 16 * lane, v);
     __builtin_amdgcn_wave_barrier();
   }
-  __device__ __forceinline__ int byte_at(int64_t i) {
+  __device__ __forceinline__ int byte_at(Ix i) {
     if (i < in_base || i >= in_base + kInStage) stage(i);
     return lds_ptr(sh->in)[i - in_base];
   }
   // the 4 bytes at i (staged window; bytes past the block are never used)
-  __device__ __forceinline__ uint32_t word_at(int64_t i) {
+  __device__ __forceinline__ uint32_t word_at(Ix i) {
     if (i < in_base || i + 4 > in_base + kInStage) stage(i);
     const uint32_t o = (uint32_t)(i - in_base);
     const PQG_L uint32_t* W = (const PQG_L uint32_t*)lds_ptr(sh->in);
-    return __builtin_amdgcn_alignbit(W[(o >> 2) + 1], W[o >> 2], (o & 3) * 8);
+    return __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbit(W[(o >> 2) + 1], W[o >> 2], (o & 3) * 8));
   }
   // at least k (<= 32) bits in the buffer; false past the end of the block.
   // Whole bytes are taken up to 4 at a time (one LDS read per refill, not one
@@ -132,7 +178,7 @@ struct Inflater {
       if (pos >= n) return false;
       int m = (64 - bitcnt) >> 3;
       m = m > 4 ? 4 : m;
-      if ((int64_t)m > n - pos) m = (int)(n - pos);
+      if ((Ix)m > n - pos) m = (int)(n - pos);
       const uint32_t x = word_at(pos);
       bitbuf |= (uint64_t)(m >= 4 ? x : (x & ((1u << (8 * m)) - 1))) << bitcnt;
       pos += m;
@@ -159,36 +205,48 @@ struct Inflater {
   // Canonical code from lengths[0..n) (RFC 1951 3.2.2): counts, symbols, and
   // the 9-bit fast table.  Returns the number of unused code points at the
   // longest length (< 0: over-subscribed, 0: complete, > 0: incomplete), as
-  // puff's construct.
+  // puff's construct.  Counts and the symbol order come from ballots over 64
+  // symbols at a time (nsym <= 288); lane l keeps the count and the running
+  // offset of length l, so no per-length arrays sit in scalar registers.
   __device__ __forceinline__ int build(Huff& h, const uint16_t* lengths, int nsym) {
     PQG_L Huff* H = lds_ptr(&h);
-    // counts (every lane, the same: n <= 288, cheap next to the block's symbols)
-    uint32_t cnt[16];
+    const uint64_t lt = (1ull << lane) - 1;  // the lanes below this one
+    uint32_t my_cnt = 0;                     // lane l: symbols of length l
+#pragma unroll 1
+    for (int k = 0; k < nsym; k += 64) {
+      const uint32_t L = k + lane < nsym ? (uint32_t)lds_ptr(lengths)[k + lane] : 16u;  // 16: no symbol
 #pragma unroll
-    for (int l = 0; l < 16; l++) cnt[l] = 0;
-    for (int s = 0; s < nsym; s++) {
-      const uint32_t L = lds_ptr(lengths)[s];
-#pragma unroll
-      for (int l = 0; l < 16; l++) cnt[l] += L == (uint32_t)l;
+      for (int l = 0; l < 16; l++) {
+        const uint32_t c = (uint32_t)__popcll(__ballot(L == (uint32_t)l));
+        if (lane == l) my_cnt += c;
+      }
     }
+    // left = 2^15 - sum_l cnt[l] * 2^(15 - l), the unused code points
     int left = 1;
-    for (int l = 1; l < 16; l++) {
-      left <<= 1;
-      left -= (int)cnt[l];
-    }
 #pragma unroll
-    for (int l = 0; l < 16; l++)
-      if (lane == l) H->count[l] = (uint16_t)cnt[l];
+    for (int l = 1; l < 16; l++) left = 2 * left - (int)__builtin_amdgcn_readlane(my_cnt, l);
+    if (lane < 16) H->count[lane] = (uint16_t)my_cnt;
+    // my_off (lane l >= 1): the first slot of length l = the counts of lengths 1 .. l-1
+    uint32_t my_off = 0;
+#pragma unroll
+    for (int l = 1; l < 15; l++) {
+      const uint32_t c = __builtin_amdgcn_readlane(my_cnt, l);
+      if (lane > l) my_off += c;
+    }
     // symbols by length then value: symbol s of length L goes after every
     // shorter code and every smaller symbol of length L
-    for (int s = lane; s < nsym; s += 64) {
-      const uint32_t L = lds_ptr(lengths)[s];
-      if (L == 0) continue;
-      uint32_t at = 0;
+#pragma unroll 1
+    for (int k = 0; k < nsym; k += 64) {
+      const uint32_t L = k + lane < nsym ? (uint32_t)lds_ptr(lengths)[k + lane] : 16u;
+      const uint32_t base = (uint32_t)__shfl((int)my_off, (int)(L & 15), 64);
+      uint32_t rank = 0;
 #pragma unroll
-      for (int l = 1; l < 16; l++) at += (uint32_t)l < L ? cnt[l] : 0u;
-      for (int t = 0; t < s; t++) at += lds_ptr(lengths)[t] == L;
-      H->symbol[at] = (uint16_t)s;
+      for (int l = 1; l < 16; l++) {
+        const uint64_t m = __ballot(L == (uint32_t)l);
+        if (L == (uint32_t)l) rank = (uint32_t)__popcll(m & lt);
+        if (lane == l) my_off += (uint32_t)__popcll(m);
+      }
+      if (L - 1u < 15u) H->symbol[base + rank] = (uint16_t)(k + lane);
     }
     __builtin_amdgcn_wave_barrier();
     // fast table: entry x = the next 9 stream bits (LSB first)
@@ -197,7 +255,7 @@ struct Inflater {
       uint16_t e = 0;
       for (int l = 1; l <= kFastBits; l++) {
         code |= (x >> (l - 1)) & 1;
-        const int c = (int)cnt[l];
+        const int c = (int)H->count[l];
         if (code - c < first) {
           e = (uint16_t)(l << 9 | H->symbol[index + (code - first)]);
           break;
@@ -218,7 +276,7 @@ struct Inflater {
     const PQG_L Huff* H = lds_ptr(&h);
     need(kFastBits);  // as many as the block holds
     if (bitcnt >= kFastBits || bitcnt > 0) {
-      const uint32_t e = H->fast[(uint32_t)bitbuf & ((1u << kFastBits) - 1)];
+      const uint32_t e = __builtin_amdgcn_readfirstlane(H->fast[(uint32_t)bitbuf & ((1u << kFastBits) - 1)]);
       const int l = (int)(e >> 9);
       if (e != 0 && l <= bitcnt) {
         bitbuf >>= l;
@@ -227,13 +285,15 @@ struct Inflater {
       }
     }
     // the slow walk, bit by bit (codes longer than 9 bits, or the block's end)
+    PQG_CNT(3, 1);
     int code = 0, first = 0, index = 0;
     for (int l = 1; l < 16; l++) {
+      PQG_CNT(4, 1);
       uint32_t b;
       if (!bits(1, &b)) return -1;
       code |= (int)b;
-      const int c = H->count[l];
-      if (code - c < first) return H->symbol[index + (code - first)];
+      const int c = __builtin_amdgcn_readfirstlane(H->count[l]);
+      if (code - c < first) return __builtin_amdgcn_readfirstlane(H->symbol[index + (code - first)]);
       index += c;
       first += c;
       first <<= 1;
@@ -243,22 +303,23 @@ struct Inflater {
   }
 
   // ---- output: the history ring, flushed to HBM (bytes below cap) and CRC'd
-  __device__ __forceinline__ void flush_to(int64_t upto) {
+  __device__ __forceinline__ void flush_to(Ix upto) {
     PQG_L uint8_t* ring = lds_ptr(sh->ring);
     __builtin_amdgcn_wave_barrier();
-    const int64_t nb = upto - flushed;
+    const Ix nb = upto - flushed;
     if (nb <= 0) return;
+    PQG_T(tf0);
     // stores: bytes [flushed, upto) below cap, 16-byte granules of the output
-    const int64_t s_hi = upto < cap ? upto : cap;
+    const Ix s_hi = upto < cap ? upto : cap;
     if (s_hi > flushed) {
-      const int64_t g0 = flushed & ~(int64_t)15;
-      for (int64_t g = g0 + 16 * (int64_t)lane; g < s_hi; g += 1024) {
+      const Ix g0 = flushed & ~(Ix)15;
+      for (Ix g = g0 + 16 * (Ix)lane; g < s_hi; g += 1024) {
         uint32_t w[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           uint32_t x = 0;
 #pragma unroll
-          for (int b = 0; b < 4; b++) x |= (uint32_t)ring[(g + 4 * k + b) & (kRing - 1)] << (8 * b);
+          for (int b = 0; b < 4; b++) x |= (uint32_t)ring[(g + 4 * k + b) & (kRingT - 1)] << (8 * b);
           w[k] = x;
         }
         if (g >= flushed && g + 16 <= s_hi && ((uintptr_t)(dst + g) & 15) == 0) {
@@ -270,16 +331,16 @@ struct Inflater {
       }
     }
     // CRC-32 of [flushed, upto): lane slices, combined in a tree
-    const int64_t per = (nb + 63) / 64;
-    const int64_t lo = flushed + per * lane, hi = lo + per < upto ? lo + per : upto;
+    const Ix per = (nb + 63) / 64;
+    const Ix lo = flushed + per * lane, hi = lo + per < upto ? lo + per : upto;
     uint32_t c = 0;  // raw (unconditioned) CRC register of the slice
-    for (int64_t i = lo; i < hi; i++) c = lds_ptr(sh->crc_tab)[(c ^ ring[i & (kRing - 1)]) & 0xff] ^ (c >> 8);
+    for (Ix i = lo; i < hi; i++) c = lds_ptr(sh->crc_tab)[(c ^ ring[i & (kRingT - 1)]) & 0xff] ^ (c >> 8);
     // combine: crc(A || B) = crc(A) * x^(8 |B|) ^ crc(B) for raw registers
-    int64_t len = hi > lo ? hi - lo : 0;
-#pragma unroll
+    Ix len = hi > lo ? hi - lo : 0;
+#pragma unroll 1
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t oc = (uint32_t)__shfl_down((int)c, o, 64);
-      const int64_t ol = __shfl_down(len, o, 64);
+      const Ix ol = __shfl_down(len, o, 64);
       if ((lane & (2 * o - 1)) == 0 && lane + o < 64) {
         c = multmodp(x8nmodp((uint64_t)ol), c) ^ oc;
         len += ol;
@@ -289,32 +350,64 @@ struct Inflater {
     // the member's conditioned CRC: crc' = ~( (~crc) * x^(8 nb) ^ raw )
     crc = ~(multmodp(x8nmodp((uint64_t)nb), ~crc) ^ slice);
     flushed = upto;
+#ifdef PQG_PROFILE
+    PQG_T(tf1);
+    PQG_CNT(5, tf1 - tf0);
+#endif
     __builtin_amdgcn_wave_barrier();
   }
-  __device__ __forceinline__ void maybe_flush() {
-    if (d - flushed >= kFlush) flush_to(d);
+  // false: a 32-bit decoder is past 2^30 decoded bytes (the 64-bit pass takes the page)
+  __device__ __forceinline__ bool maybe_flush() {
+    if (d - flushed >= kFlushT) {
+      if (sizeof(Ix) < 8 && d > (Ix)(1 << 30)) return false;
+      flush_to(d);
+    }
+    return true;
   }
   __device__ __forceinline__ void put(uint32_t byte) {
-    if (lane == 0) lds_ptr(sh->ring)[d & (kRing - 1)] = (uint8_t)byte;
+    if (lane == 0) lds_ptr(sh->ring)[d & (kRingT - 1)] = (uint8_t)byte;
     d++;
   }
-  // len bytes from dist back (dist <= bytes of this member so far)
-  __device__ __forceinline__ void copy(uint32_t dist, uint32_t len) {
+  // len bytes from dist back (dist <= bytes of this member so far); false: a
+  // source byte is neither in the ring nor stored (the 32 KiB-ring pass takes the page)
+  __device__ __forceinline__ bool copy(uint32_t dist, uint32_t len) {
     PQG_L uint8_t* ring = lds_ptr(sh->ring);
     __builtin_amdgcn_wave_barrier();
     uint32_t done = 0;
+    if (kRingT < 32768 && dist > (uint32_t)(kRingT - 64)) {
+      // older than the ring: flushed (flushed >= d - kFlushT - 258), read back
+      // from the output after this wave's stores completed (L2-coherent loads)
+      __builtin_amdgcn_s_waitcnt(0);
+      while (done < len) {
+        const uint32_t k = len - done < 64u ? len - done : 64u;
+        const Ix sp = d + done - dist + lane;  // source byte
+        if (__ballot((uint32_t)lane < k && sp >= cap)) return false;
+        uint32_t v = 0;
+        if ((uint32_t)lane < k) {
+          const uintptr_t a = (uintptr_t)(dst + sp);
+          const uint32_t wv = ld_l2_u32((const PQG_G uint32_t*)(a & ~(uintptr_t)3));
+          v = (wv >> (8 * (a & 3))) & 0xff;
+        }
+        if ((uint32_t)lane < k) ring[(d + done + lane) & (kRingT - 1)] = (uint8_t)v;
+        __builtin_amdgcn_wave_barrier();
+        done += k;
+      }
+      d += len;
+      return true;
+    }
     while (done < len) {
       // a round of min(dist, 64) bytes never reads a byte written in the round
       const uint32_t step = dist < 64u ? dist : 64u;
       const uint32_t k = len - done < step ? len - done : step;
       uint8_t v = 0;
-      if ((uint32_t)lane < k) v = ring[(d + done + lane - dist) & (kRing - 1)];
+      if ((uint32_t)lane < k) v = ring[(d + done + lane - dist) & (kRingT - 1)];
       __builtin_amdgcn_wave_barrier();
-      if ((uint32_t)lane < k) ring[(d + done + lane) & (kRing - 1)] = v;
+      if ((uint32_t)lane < k) ring[(d + done + lane) & (kRingT - 1)] = v;
       __builtin_amdgcn_wave_barrier();
       done += k;
     }
     d += len;
+    return true;
   }
 
   // ---- one DEFLATE stream (RFC 1951 3.2.3), kOK or kGZIP
@@ -323,6 +416,7 @@ struct Inflater {
       const int sym = decode(lc);
       if (sym < 0) return kGZIP;
       if (sym < 256) {
+        PQG_CNT(0, 1);
         put((uint32_t)sym);
       } else if (sym == 256) {
         return kOK;
@@ -330,16 +424,21 @@ struct Inflater {
         const int s = sym - 257;
         if (s >= 29) return kGZIP;
         uint32_t e;
-        if (!bits(kLenExt[s], &e)) return kGZIP;
-        const uint32_t len = kLenBase[s] + e;
+        const uint32_t lx = len_ext((uint32_t)s);
+        if (!bits(lx, &e)) return kGZIP;
+        const uint32_t len = len_base((uint32_t)s, lx) + e;
         const int ds = decode(dc);
         if (ds < 0 || ds >= 30) return kGZIP;
-        if (!bits(kDistExt[ds], &e)) return kGZIP;
-        const uint32_t dist = kDistBase[ds] + e;
-        if ((int64_t)dist > d - mstart) return kGZIP;  // "invalid distance too far back"
-        copy(dist, len);
+        const uint32_t dx = dist_ext((uint32_t)ds);
+        if (!bits(dx, &e)) return kGZIP;
+        const uint32_t dist = dist_base((uint32_t)ds, dx) + e;
+        if ((Ix)dist > d - mstart) return kGZIP;  // "invalid distance too far back"
+        PQG_CNT(1, 1);
+        PQG_CNT(2, dist > (uint32_t)(kRingT - 64) ? 1 : 0);
+        PQG_CNT(7, len);
+        if (!copy(dist, len)) return kInflateRedo;
       }
-      maybe_flush();
+      if (!maybe_flush()) return kInflateRedo;
     }
   }
   __device__ __forceinline__ int stored() {
@@ -352,19 +451,32 @@ struct Inflater {
       uint32_t v;
       if (!bits(8, &v)) return kGZIP;
       put(v);
-      if ((k & 255) == 255) maybe_flush();
+      if (((k & 255) == 255 || k + 1 == len) && !maybe_flush()) return kInflateRedo;
     }
-    maybe_flush();
     return kOK;
   }
+  // the block's code tables (codes() then decodes its symbols: one inlined copy)
   __device__ __forceinline__ int fixed() {
     PQG_L uint16_t* L = lds_ptr(sh->lens);
     for (int s = lane; s < 288 + 30; s += 64)
       L[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
     __builtin_amdgcn_wave_barrier();
-    build(sh->lit, sh->lens, 288);
-    build(sh->dist, sh->lens + 288, 30);
-    return codes(sh->lit, sh->dist);
+    return tables(288, 30, false);
+  }
+  // the literal/length and distance codes from lens[0..nlen) and lens[288..):
+  // one build site in a loop (not one inlined build per table).  check: a
+  // dynamic block's codes must be complete, except that a code may be a
+  // single code of length 1 (puff, zlib's inflate_table); the fixed distance
+  // code (30 of 32 five-bit codes) is incomplete by definition.
+  __device__ __forceinline__ int tables(uint32_t nlen, uint32_t ndist, bool check) {
+#pragma unroll 1
+    for (int t = 0; t < 2; t++) {
+      Huff& h = t ? sh->dist : sh->lit;
+      const int ns = (int)(t ? ndist : nlen);
+      const int e = build(h, sh->lens + (t ? 288 : 0), ns);
+      if (check && (e < 0 || (e > 0 && ns != (int)lds_ptr(h.count)[0] + (int)lds_ptr(h.count)[1]))) return kGZIP;
+    }
+    return kOK;
   }
   __device__ __forceinline__ int dynamic() {
     uint32_t nlen, ndist, ncode;
@@ -432,24 +544,19 @@ struct Inflater {
       else if (s < total) L[288 + (s - nlen)] = v[k];
     }
     __builtin_amdgcn_wave_barrier();
-    // incomplete codes only when all codes have length <= 1 (one code of
-    // length 1: puff, zlib's inflate_table)
-    const int el = build(sh->lit, sh->lens, (int)nlen);
-    if (el < 0 || (el > 0 && (int)nlen != (int)lds_ptr(sh->lit.count)[0] + (int)lds_ptr(sh->lit.count)[1])) return kGZIP;
-    const int ed = build(sh->dist, sh->lens + 288, (int)ndist);
-    if (ed < 0 || (ed > 0 && (int)ndist != (int)lds_ptr(sh->dist.count)[0] + (int)lds_ptr(sh->dist.count)[1]))
-      return kGZIP;
-    return codes(sh->lit, sh->dist);
+    return tables(nlen, ndist, true);
   }
   __device__ __forceinline__ int deflate() {
     uint32_t last, type;
     do {
       if (!bits(1, &last) || !bits(2, &type)) return kGZIP;
       int e;
-      if (type == 0) e = stored();
-      else if (type == 1) e = fixed();
-      else if (type == 2) e = dynamic();
-      else e = kGZIP;
+      if (type == 0) {
+        e = stored();
+      } else {
+        e = type == 1 ? fixed() : type == 2 ? dynamic() : kGZIP;
+        if (!e) e = codes(sh->lit, sh->dist);
+      }
       if (e) return e;
     } while (!last);
     return kOK;
@@ -535,9 +642,12 @@ __device__ __forceinline__ void gzip_loc(const PageDev& pg, int64_t* src_off, in
   *ulen = (int64_t)pg.usize - lv;
 }
 
-__global__ void __launch_bounds__(64) k_inflate(JobDev* jobs, PageDev* pages, const int* list, const int* total,
-                                                int* queue, uint8_t* scratch) {
-  __shared__ __attribute__((aligned(16))) InflateShared sh;
+// mode 0: every GZIP page of the list; 1: only the pages k_inflate_s left
+// (kPageInflateRedo).
+template <int kRingT, typename Ix>
+__device__ __forceinline__ void inflate_pages(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+                                              int* queue, uint8_t* scratch, int mode) {
+  __shared__ __attribute__((aligned(16))) InflateShared<kRingT> sh;
   const int lane = lane_id();
   for (;;) {
     const int t = queue_next(queue);
@@ -545,18 +655,32 @@ __global__ void __launch_bounds__(64) k_inflate(JobDev* jobs, PageDev* pages, co
     const int pidx = __builtin_amdgcn_readfirstlane(list[t]);
     const PageDev pg = pages[pidx];
     if (pg.read_status != kOK || pg.scratch_offset < 0) continue;
+    if (mode == 1 && !(pg.flags & kPageInflateRedo)) continue;
     const JobDev job = jobs[pg.job];
     if (job.codec != kCodecGzip) continue;
     int64_t so, clen, ulen;
     gzip_loc(pg, &so, &clen, &ulen);
-    Inflater f;
+    Inflater<kRingT, Ix> f;
     f.sh = &sh;
     f.src = gconst(job.data) + so;
     f.n = clen;
     f.dst = gmut(scratch) + job.scratch_base + pg.scratch_offset;
     f.cap = ulen;
     f.lane = lane;
+    PQG_T(tp0);
     int e = f.run();
+#ifdef PQG_PROFILE
+    PQG_T(tp1);
+    if (kRingT < kRing) {
+      PQG_ACC(8, tp0, tp1);
+      PQG_ACC(9, 0, 1);
+      for (int k = 0; k < 8; k++) PQG_ACC(k, 0, f.f_cnt[k]);
+    }
+#endif
+    if (e == kInflateRedo) {  // k_inflate (32 KiB ring) decodes it again
+      if (lane == 0) pages[pidx].flags |= kPageInflateRedo;
+      continue;
+    }
     if (pg.flags & kPageBareBlock) {  // pqg_block_decompress: the decoded length, no size check
       if (lane == 0) pages[pidx].gz_len = f.d;
     } else if (e == kOK && f.d != ulen) {
@@ -566,6 +690,21 @@ __global__ void __launch_bounds__(64) k_inflate(JobDev* jobs, PageDev* pages, co
     if (e == kOK && pg.page_type == 0 && !values_supported(job.type, job.type_length, pg.encoding)) e = kUNSUPPORTED;
     if (lane == 0 && e != kOK) pages[pidx].read_status = e;
   }
+}
+
+// the 32 KiB ring: pqg_block_decompress blocks (mode 0) and the pages
+// k_inflate_s left (mode 1)
+__global__ void __launch_bounds__(64) k_inflate(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+                                                int* queue, uint8_t* scratch, int mode) {
+  inflate_pages<kRing, int64_t>(jobs, pages, list, total, queue, scratch, mode);
+}
+// the GZIP pages of a decode, kRingSmall-byte ring
+#ifndef PQG_INFLATE_WPE
+#define PQG_INFLATE_WPE 1
+#endif
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, 64), amdgpu_waves_per_eu(PQG_INFLATE_WPE))) k_inflate_s(JobDev* jobs, PageDev* pages, const int* list, const int* total,
+                                                  int* queue, uint8_t* scratch) {
+  inflate_pages<kRingSmall, int32_t>(jobs, pages, list, total, queue, scratch, 0);
 }
 
 }  // namespace pqg

@@ -45,7 +45,9 @@ __global__ void k_page_list(JobDev* jobs, PageDev* pages, int n_jobs, int* list,
 __global__ void k_snappy(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
                          uint8_t* scratch);
 __global__ void k_inflate(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
-                          uint8_t* scratch);
+                          uint8_t* scratch, int mode);
+__global__ void k_inflate_s(JobDev* jobs, PageDev* pages, const int* list, const int* total, int* queue,
+                            uint8_t* scratch);
 __global__ void k_snap_plan(const JobDev* jobs, PageDev* pages, const int* list, const int* total, int* ctr,
                             SnapSub* subs, int sub_cap, int* seg_page, int seg_cap);
 __global__ void k_snap_seg(const JobDev* jobs, const PageDev* pages, const int* seg_page, const int* seg_total,
@@ -99,6 +101,7 @@ int prof_read_levels(unsigned long long* out);
 int prof_read_strings(unsigned long long* out);
 int prof_read_snappy(unsigned long long* out);
 int prof_read_dict(unsigned long long* out);
+int prof_read_inflate(unsigned long long* out);
 }  // namespace pqg
 #endif
 
@@ -185,6 +188,7 @@ struct pqg_ctx {
   int levlong_waves = 28; // PQG_LEVLONG_WAVES: k_level_long waves per CU (66 VGPRs: 7 per SIMD; 8: C5 0.61 ms, 28: 0.32)
   int link_waves = 16;    // PQG_LINK_WAVES: k_snap_link waves per CU (one wave per big page; 4: C4 +50 %)
   int snappy_per_cu = 2;  // resident k_snappy waves per CU (LDS-bound: the output history ring)
+  int inflate_per_cu = 8; // resident k_inflate_s waves per CU (LDS / VGPR bound), from the occupancy query
   DevBuf jobs, pages, list, counters, def_arena, rep_arena, value_arena, scratch;
   DevBuf tile_job;  // K1: tile -> job
   DevBuf tile_count, tile_okc, tile_off, tile_okoff, cand_pos, cands, succ, idx2slot, ok2slot, order;  // K1
@@ -291,6 +295,10 @@ int pqg_ctx_create(int device, pqg_ctx** out) {
           hipSuccess &&
       occ > 0)
     c->snappy_per_cu = occ;
+  occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(&k_inflate_s), 64, 0) ==
+          hipSuccess && occ > 0)
+    c->inflate_per_cu = occ;
   // counters: ctr[0..1023] + the kQShards-sharded work queues and the per-stage flags
   if (c->counters.grow(sizeof(int) * (size_t)(1024 + kQueueSlots * kQueueInts))) {
     pqg_ctx_destroy(c);
@@ -565,9 +573,12 @@ static int launch_pipeline(pqg_ctx* c) {
                        (int)std::min<int64_t>(c->sn_seg_cap, INT32_MAX), (uint2*)c->sn_F.p};
     launch_snappy(c, s, jobs, pages, list, ctr, c->list_cap, ctr + 32, Q(0), Q(kQueueSnapSerial), scratch, T);
   }
-  if (any_gzip)  // one wave per GZIP page (pqg_inflate.hip)
-    hipLaunchKernelGGL(k_inflate, dim3(qgrid(c->num_cus * 4)), dim3(64), 0, s, jobs, pages, list, ctr, Q(kQueueInflate),
-                       scratch);
+  if (any_gzip) {  // one wave per GZIP page (pqg_inflate.hip): the 8 KiB ring, then the pages it left
+    hipLaunchKernelGGL(k_inflate_s, dim3(qgrid(c->num_cus * c->inflate_per_cu)), dim3(64), 0, s, jobs, pages, list, ctr,
+                       Q(kQueueInflate), scratch);
+    hipLaunchKernelGGL(k_inflate, dim3(qgrid(c->num_cus * 4)), dim3(64), 0, s, jobs, pages, list, ctr,
+                       Q(kQueueInflateRedo), scratch, 1);
+  }
   if (c->timed) hipEventRecord(c->ev[3], s);
   HStream* streams = (HStream*)c->streams.p;
   RunEnt* runs = (RunEnt*)c->runs.p;
@@ -892,7 +903,7 @@ static int inflate_pass(pqg_ctx* c, int64_t n, int64_t store, PageDev* out) {
       hipMemsetAsync(ints + 4, 0, sizeof(int) * kQueueInts, c->stream) != hipSuccess)
     return PQG_ERR_HIP;
   hipLaunchKernelGGL(k_inflate, dim3(qgrid(1)), dim3(64), 0, c->stream, djob, dpage, ints, ints + 1, ints + 4,
-                     (uint8_t*)c->blk_dst.p);
+                     (uint8_t*)c->blk_dst.p, 0);
   if (hipGetLastError() != hipSuccess) return PQG_ERR_HIP;
   if (hipMemcpyAsync(out, dpage, sizeof(PageDev), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
@@ -1066,13 +1077,18 @@ int pqg_debug_counters(pqg_ctx* c, uint64_t* out, int cap) {
 #ifdef PQG_PROFILE
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
-  unsigned long long a[64], b[64], c3[64], d4[64], e5[64];
+  unsigned long long a[64], b[64], c3[64], d4[64], e5[64], f6[64];
   if (pqg::prof_read_values(a) || pqg::prof_read_levels(b) || pqg::prof_read_strings(c3) ||
-      pqg::prof_read_snappy(d4) || pqg::prof_read_dict(e5))
+      pqg::prof_read_snappy(d4) || pqg::prof_read_dict(e5) || pqg::prof_read_inflate(f6))
     return PQG_ERR_HIP;
   int k = 0;
-  for (; k < 160 && k < cap; k++)
-    out[k] = k < 32 ? a[k] : k < 64 ? b[k - 32] : k < 96 ? c3[k - 64] : k < 128 ? d4[k - 96] : e5[k - 128];
+  for (; k < 192 && k < cap; k++)
+    out[k] = k < 32    ? a[k]
+             : k < 64  ? b[k - 32]
+             : k < 96  ? c3[k - 64]
+             : k < 128 ? d4[k - 96]
+             : k < 160 ? e5[k - 128]
+                       : f6[k - 160];
   return k;
 #else
   return 0;

@@ -314,3 +314,52 @@ def test_gpu_gzip_name_bound(dec, name_len, comment_len, want):
     assert rc == (abi.STATUS_CODES[want] if want else 0), abi.status_name(rc)
     if not want:
         assert dst[:n].tobytes() == raw
+
+
+REDO = 64  # PQG_PAGE_FLAG_INFLATE_REDO
+
+
+def _far_raw(n=12000, reps=3, seed=45):
+    """Random bytes repeated: every match reaches n bytes back, past the 8 KiB ring."""
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, 256, n, dtype=np.uint8).tobytes() * reps
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["far", "far_near", "text_window", "far_members", "far_fixed"])
+def test_gpu_gzip_far_matches(dec, name):
+    """k_inflate_s keeps 8 KiB of history in LDS; matches reaching further
+    (up to the 32 KiB window) read their bytes back from the page's stored
+    output.  Bit-exact against the oracle; no page needs the 32 KiB pass."""
+    import parity as P
+    rng = np.random.default_rng(46)
+    far = _far_raw()
+    raw = {"far": far,
+           "far_near": b"".join(far[i:i + 3000] + bytes(rng.integers(0, 4, 500, dtype=np.uint8))
+                                for i in range(0, 36000, 3000)),
+           "text_window": b" ".join(b"v%d" % int(i) for i in rng.integers(0, 9000, 40000)),
+           "far_members": far + far,
+           "far_fixed": far}[name]
+    raw = raw[: len(raw) // 8 * 8]
+    gz = {"far_members": gzip.compress(far) + gzip.compress(far),
+          "far_fixed": _zlib_gzip(raw, 6, zlib.Z_FIXED)}.get(name) or _zlib_gzip(raw, 9)
+    exp, got = P.compare_chunk_bytes(_gz_page(raw, gz, len(raw) // 8), dec, ptype=abi.INT64, codec=abi.CODEC_GZIP)
+    assert exp.status == 0
+    assert not any(p.flags & REDO for p in got.pages)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("short", [8, 4000, 12008, 23992])
+def test_gpu_gzip_far_match_past_size(dec, short):
+    """A page that decodes to more than its uncompressed size: bytes past the
+    size are never stored, so a far match reading one sends the page to the
+    32 KiB-ring pass, which reports the same status as the oracle (SIZE)."""
+    import parity as P
+    raw = _far_raw()
+    gz = _zlib_gzip(raw, 9)
+    ulen = len(raw) - short
+    page = U.page_header_v1(ulen, len(gz), ulen // 8, abi.ENC_PLAIN) + gz
+    exp, got = P.compare_chunk_bytes(page, dec, ptype=abi.INT64, codec=abi.CODEC_GZIP)
+    assert exp.status == abi.STATUS_CODES["SIZE"], abi.status_name(exp.status)
+    # a far match reads bytes 12000 back: past the size when the size ends before 24000
+    assert bool(any(p.flags & REDO for p in got.pages)) == (ulen < 24000)

@@ -16,6 +16,8 @@ cfg = sys.argv[2] if len(sys.argv) > 2 else "c2"
 if cfg.startswith("c2"):  # c2 (every width) or c2:b1,b2,... (those widths)
     bits = [int(b) for b in cfg[3:].split(",")] if ":" in cfg else [1, 2, 4, 8, 12, 16, 20]
     files = [f[1] for f in W.config_c2_family(rows=rows, bits_list=bits)]
+elif cfg == "c3_gzip":
+    files = [W.config_c3(rows=rows, codec=W.GZIP)[0]]
 elif cfg == "c4":
     files = [W.config_c4(rows=rows)[0]]
 else:
@@ -28,9 +30,9 @@ for data in files:
     jobs.append(pqgpu.device_job(pf, 0, 0, dev))
 arr = (abi.ChunkJob * len(jobs))(*jobs)
 res = (abi.ChunkResult * len(jobs))()
-out = (C.c_uint64 * 160)()
+out = (C.c_uint64 * 192)()
 for it in range(3):
     assert dec.L.pqg_decode_chunks(dec.ctx, arr, len(jobs), res) == 0
-    k = dec.L.pqg_debug_counters(dec.ctx, out, 160)
+    k = dec.L.pqg_debug_counters(dec.ctx, out, 192)
     print("iter", it, "timings", ["%.3f" % x for x in dec.timings()])
     print("  counters", {i: out[i] for i in range(k) if out[i]})
