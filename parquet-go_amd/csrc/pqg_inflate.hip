@@ -54,7 +54,7 @@ constexpr uint32_t kCrcPoly = 0xedb88320u;  // CRC-32 (IEEE, reflected): gzip tr
 struct Huff {
   uint16_t count[16];    // codes per length
   uint16_t symbol[288];  // symbols by (length, value)
-  uint16_t fast[1 << kFastBits];  // next 9 stream bits -> (length << 9) | symbol, 0: longer code
+  uint16_t fast[1 << kFastBits];  // next 9 stream bits -> literal << 15 | length << 9 | symbol, 0: longer code
 };
 
 template <int kRingT>
@@ -257,7 +257,8 @@ struct Inflater {
         code |= (x >> (l - 1)) & 1;
         const int c = (int)H->count[l];
         if (code - c < first) {
-          e = (uint16_t)(l << 9 | H->symbol[index + (code - first)]);
+          const uint32_t sy = H->symbol[index + (code - first)];
+          e = (uint16_t)((sy < 256 ? 0x8000u : 0u) | l << 9 | sy);
           break;
         }
         index += c;
@@ -277,7 +278,7 @@ struct Inflater {
     need(kFastBits);  // as many as the block holds
     if (bitcnt >= kFastBits || bitcnt > 0) {
       const uint32_t e = __builtin_amdgcn_readfirstlane(H->fast[(uint32_t)bitbuf & ((1u << kFastBits) - 1)]);
-      const int l = (int)(e >> 9);
+      const int l = (int)((e >> 9) & 15);
       if (e != 0 && l <= bitcnt) {
         bitbuf >>= l;
         bitcnt -= l;
@@ -411,8 +412,49 @@ struct Inflater {
   }
 
   // ---- one DEFLATE stream (RFC 1951 3.2.3), kOK or kGZIP
+  // Literals while the next code is a literal of the fast table: the bytes
+  // collect in one VGPR (lane i: the batch's i-th literal) and go to the ring
+  // 64 at a time, so a literal costs one table read and a few scalar ops
+  // instead of decode() + put().  Exact: only real stream bits are consumed
+  // (the 4-byte refills stop short of the end, where decode() takes over),
+  // and any other symbol is left to decode(), which reads the same entry.
+  // Returns with fewer than kFlushT + 64 bytes unflushed.
+  __device__ __forceinline__ void lit_run(const Huff& lc) {
+    const PQG_L uint16_t* F = lds_ptr(lc.fast);
+    PQG_L uint8_t* ring = lds_ptr(sh->ring);
+    int pend = 0;
+    int np = 0;
+    for (;;) {
+      if (bitcnt < 32) {
+        if (pos + 4 <= n) {
+          bitbuf |= (uint64_t)word_at(pos) << bitcnt;
+          pos += 4;
+          bitcnt += 32;
+        } else if (bitcnt < kFastBits) {
+          break;
+        }
+      }
+      const uint32_t e = __builtin_amdgcn_readfirstlane(F[(uint32_t)bitbuf & ((1u << kFastBits) - 1)]);
+      if (!(e & 0x8000u)) break;  // not a literal of the table (a longer code, or a length / end code)
+      const uint32_t l = (e >> 9) & 15;
+      bitbuf >>= l;
+      bitcnt -= (int)l;
+      PQG_CNT(0, 1);
+      pend = lane == np ? (int)(e & 255) : pend;  // lane np takes the byte
+      if (++np == 64) {
+        ring[(d + lane) & (kRingT - 1)] = (uint8_t)pend;
+        d += 64;
+        np = 0;
+        if (d - flushed >= kFlushT) break;
+      }
+    }
+    if (lane < np) ring[(d + lane) & (kRingT - 1)] = (uint8_t)pend;
+    d += np;
+    __builtin_amdgcn_wave_barrier();
+  }
   __device__ __forceinline__ int codes(const Huff& lc, const Huff& dc) {
     for (;;) {
+      lit_run(lc);
       const int sym = decode(lc);
       if (sym < 0) return kGZIP;
       if (sym < 256) {
