@@ -425,12 +425,13 @@ struct Inflater {
     int pend = 0;
     int np = 0;
     for (;;) {
+      // two literals per step: >= 2 x 9 bits in the buffer
       if (bitcnt < 32) {
         if (pos + 4 <= n) {
           bitbuf |= (uint64_t)word_at(pos) << bitcnt;
           pos += 4;
           bitcnt += 32;
-        } else if (bitcnt < kFastBits) {
+        } else if (bitcnt < 2 * kFastBits) {
           break;
         }
       }
@@ -441,7 +442,18 @@ struct Inflater {
       bitcnt -= (int)l;
       PQG_CNT(0, 1);
       pend = lane == np ? (int)(e & 255) : pend;  // lane np takes the byte
-      if (++np == 64) {
+      const uint32_t e2 = __builtin_amdgcn_readfirstlane(F[(uint32_t)bitbuf & ((1u << kFastBits) - 1)]);
+      if (!(e2 & 0x8000u)) {
+        np++;
+        break;
+      }
+      const uint32_t l2 = (e2 >> 9) & 15;
+      bitbuf >>= l2;
+      bitcnt -= (int)l2;
+      PQG_CNT(0, 1);
+      pend = lane == np + 1 ? (int)(e2 & 255) : pend;
+      np += 2;
+      if (np == 64) {
         ring[(d + lane) & (kRingT - 1)] = (uint8_t)pend;
         d += 64;
         np = 0;
