@@ -43,7 +43,7 @@ for p in (ROOT, os.path.join(ROOT, "parquet-go_amd")):
 METRIC = "decoded GB/s (uncompressed output) per GPU & node at 1/2/4/8; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 STAGES = ["scan", "list", "snappy", "levels", "walk", "unused", "nn_scan", "values", "strings", "finalize"]
-PROFILE_TAG = "r05"
+PROFILE_TAG = "r06"
 
 
 def log(*a):
