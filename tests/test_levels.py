@@ -125,3 +125,44 @@ def test_level_stream_mutations(dec):
             for _ in range(int(rng.integers(1, 4))):
                 b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
             P.compare_chunk_bytes(bytes(b), dec, ptype=abi.INT32, max_def=maxd)
+
+
+def short_chain_page(rng, nruns, how):
+    """A 1-bit level stream of `nruns` runs (the writer's shape: bit-packed
+    runs of up to 63 groups, RLE runs), for the whole-page decoder's serial
+    chain walk (<= 64 runs) and the exit table past it."""
+    out, vals = bytearray(), []
+    for _ in range(nruns):
+        if rng.random() < 0.7:
+            g = int(rng.integers(1, 64))
+            vs = (rng.random(8 * g) < 0.9).astype(np.int64)
+            out += uvarint(g << 1 | 1) + bitpack(vs, 1)
+            vals += [int(x) for x in vs]
+        else:
+            cnt = int(rng.integers(1, 700))
+            v = int(rng.integers(0, 2))
+            out += uvarint(cnt << 1) + bytes([v])
+            vals += [v] * cnt
+    n = len(vals)
+    if how == "inside":  # the count ends inside the last run
+        n = max(1, n - int(rng.integers(1, 8)))
+    elif how == "short":  # the stream ends before the count (EOF)
+        n = n + int(rng.integers(1, 50))
+    elif how == "bad_after":  # a bad RLE value after the count: never read
+        out += uvarint(8 << 1) + bytes([2])
+    elif how == "bad_before":  # a bad RLE value before the count
+        out = out[:0] + uvarint(8 << 1) + bytes([2]) + out
+        n = n + 8
+    elif how == "trailing":
+        out += bytes(rng.integers(0, 256, 17, dtype=np.uint8))
+    vals_b = rng.integers(-2**31, 2**31 - 1, n, dtype=np.int64).astype("<i4").tobytes()
+    return U.v1_page(vals_b, n, 0, defs=bytes(out))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nruns", [1, 2, 40, 63, 64, 65, 90])
+@pytest.mark.parametrize("how", ["exact", "inside", "short", "bad_after", "bad_before", "trailing"])
+def test_one_bit_short_chains(dec, nruns, how):
+    rng = np.random.default_rng(1000 * nruns + len(how))
+    pages = b"".join(short_chain_page(rng, nruns, how) for _ in range(6))
+    P.compare_chunk_bytes(pages, dec, ptype=abi.INT32, max_def=1)
