@@ -142,8 +142,9 @@ struct Inflater {
   int lane;
 #ifdef PQG_PROFILE
   // 0 literals, 1 matches, 2 far matches, 3 slow decodes, 4 slow-walk bits,
-  // 5 flush cycles, 6 stage() refills, 7 match bytes
-  uint64_t f_cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // 5 flush cycles, 6 stage() refills, 7 match bytes, 8 lit_run cycles,
+  // 9 lit_run calls, 10 cycles of the other symbols (decode, copy, flush)
+  uint64_t f_cnt[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
 
   __device__ __forceinline__ void stage(Ix at) {
@@ -466,7 +467,13 @@ struct Inflater {
   }
   __device__ __forceinline__ int codes(const Huff& lc, const Huff& dc) {
     for (;;) {
+      PQG_T(tl0);
       lit_run(lc);
+#ifdef PQG_PROFILE
+      PQG_T(tl1);
+      PQG_CNT(8, tl1 - tl0);
+      PQG_CNT(9, 1);
+#endif
       const int sym = decode(lc);
       if (sym < 0) return kGZIP;
       if (sym < 256) {
@@ -493,6 +500,10 @@ struct Inflater {
         if (!copy(dist, len)) return kInflateRedo;
       }
       if (!maybe_flush()) return kInflateRedo;
+#ifdef PQG_PROFILE
+      PQG_T(tl2);
+      PQG_CNT(10, tl2 - tl1);
+#endif
     }
   }
   __device__ __forceinline__ int stored() {
@@ -729,6 +740,7 @@ __device__ __forceinline__ void inflate_pages(JobDev* jobs, PageDev* pages, cons
       PQG_ACC(8, tp0, tp1);
       PQG_ACC(9, 0, 1);
       for (int k = 0; k < 8; k++) PQG_ACC(k, 0, f.f_cnt[k]);
+      for (int k = 8; k < 11; k++) PQG_ACC(k + 2, 0, f.f_cnt[k]);  // slots 10..12
     }
 #endif
     if (e == kInflateRedo) {  // k_inflate (32 KiB ring) decodes it again
