@@ -9,15 +9,18 @@
 // than the page's uncompressed size is PQG_ERR_SIZE (compress.go:117).
 //
 // One wave per compressed page (k_inflate_s: an 8 KiB history ring, older
-// matches read back from the stored output; k_inflate: the 32 KiB window).
-// DEFLATE is a serial bit stream, so the
-// symbol decode runs wave-uniform (every lane holds the same decoder state;
-// table reads are LDS broadcasts) with canonical-Huffman tables built per
-// block in LDS (a 9-bit fast table, then the count / symbol walk of RFC 1951
-// codes); the lanes split the byte work: copies of a match from the 32 KiB
-// LDS history ring, the table builds, the flush of decoded bytes to HBM in
-// 16-byte granules, and the CRC-32 of every flushed piece (per-lane slices
-// combined in a tree with x^(8n) mod P shifts).
+// matches read back from the stored output; k_inflate: the 32 KiB window, for
+// pqg_block_decompress and the pages k_inflate_s hands back).  DEFLATE is a
+// serial bit stream, so the symbol decode runs wave-uniform (the decoder
+// state is scalar; table reads are LDS broadcasts moved to scalar registers)
+// with canonical-Huffman tables built per block in LDS by ballots (a 9-bit
+// fast table with a literal flag, then the count / symbol walk of RFC 1951
+// codes).  Runs of literals take a tight loop (lit_run: two per step, bytes
+// gathered one per lane and written to the ring 64 at a time); the lanes
+// split the byte work: copies of a match from the LDS history ring, the
+// flush of decoded bytes to HBM in 16-byte granules, and the CRC-32 of every
+// flushed piece (per-lane slices combined in a tree with x^(8n) mod P shifts
+// from a table of x^(2^k)).
 #include <hip/hip_runtime.h>
 
 #include "pqg_common.h"
